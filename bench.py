@@ -1,0 +1,174 @@
+"""Benchmark: QP instances/s of the I-ADMM-LSTM test-mode solve at BASELINE config 2.
+
+A "step" = one full test-mode solve of the per-GPU batch, already resident in HBM (the timed
+scope of main.py:825-834,881-890,1024-1031): Ruiz scaling (10 rounds) -> K=100 Stage-I
+iterations -> final unscale.  Instances: n=1000, 500 inequality + 500 equality rows, hidden 800,
+B=1024 per GPU (synthetic, restating generate_data.py:67-76; random-init weights with the
+reference's initialisation — throughput does not depend on weight values).
+
+Multi-GPU: one process per GPU (torch.distributed.run); the instance batch is sharded (rank r
+solves instances [r*B, (r+1)*B)) with no data-path collective; a barrier brackets the timed
+region and the max time over ranks is reported ("scaling": "weak").
+
+Prints ONE JSON line on rank 0, including
+  roofline      the dominant kernel (iadmm_lstm_cell_fwd, fp32 MFMA) from hipEvent timing of
+                every launch inside the timed region, plus the same for the HBM-bound residual
+                matvec (iadmm_kkt_resgrad) under "roofline_matvec";
+  cpu_baseline  the CPU oracle (oracle/iadmm_oracle.py: the reference's op structure in
+                PyTorch-CPU fp32) on a bounded sample of the same workload, rank 0 only.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "i-admm-lstm_amd"))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+
+FP32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md, Peak FP32 (matrix), spec
+HBM_PEAK_GBS = 8000.0           # MI355X_MICROARCH.md, HBM3E peak BW, spec
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=2)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--batch", type=int, default=1024, help="instances per GPU")
+    ap.add_argument("--num_var", type=int, default=1000)
+    ap.add_argument("--num_ineq", type=int, default=500)
+    ap.add_argument("--num_eq", type=int, default=500)
+    ap.add_argument("--hidden_dim", type=int, default=800)
+    ap.add_argument("--outer_T", type=int, default=100)
+    ap.add_argument("--sigma", type=float, default=6e-6)
+    ap.add_argument("--cpu-sample", type=int, default=8, help="instances in the CPU baseline (0: skip)")
+    ap.add_argument("--in-place-scaling", action="store_true",
+                    help="scale Q/A0 in place (no unscaled copy; residuals via the scaling identity)")
+    return ap.parse_args()
+
+
+def cpu_baseline(args, d, params):
+    """Oracle (reference op structure, torch-CPU fp32) on the first ``cpu_sample`` instances."""
+    from oracle import iadmm_oracle as orc
+    Bc = args.cpu_sample
+    threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+    torch.set_num_threads(threads)
+    cpu = {k: d[k][:Bc].cpu() for k in ("Q", "p", "A0", "zl", "zu")}
+    pc = {k: v.detach().cpu() for k, v in params.items()}
+    t0 = time.perf_counter()
+    with torch.no_grad():
+        out = orc.solve(pc, cpu["Q"], cpu["p"], cpu["A0"], cpu["zl"], cpu["zu"], args.num_ineq, args.num_eq,
+                        args.outer_T, args.sigma, args.hidden_dim)
+    dt = time.perf_counter() - t0
+    return dict(value=Bc / dt, unit="QP instances/s", cores=threads, kind="port",
+                sample=f"{Bc} instances x full solve (Ruiz + K={args.outer_T} + unscale), same synthetic "
+                       f"instances and weights as the GPU run, {dt:.1f} s",
+                final_primal=float(out["primal"].mean()), final_dual=float(out["dual"].mean()))
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    from iadmm import data, solver
+
+    n, mi, me, h, T, B = args.num_var, args.num_ineq, args.num_eq, args.hidden_dim, args.outer_T, args.batch
+    N = n + mi + me
+    d = data.make_qp_batch(n, mi, me, B, first_index=rank * B, device="cuda")
+    params = data.init_lstm_params(h, T, device="cuda")
+    packed = solver.PackedWeights()
+    keep = not args.in_place_scaling
+    if not keep:
+        master = {k: v.clone() for k, v in d.items()}  # restored before every step (untimed)
+
+    def step(timer):
+        if not keep:
+            for k in d:
+                d[k].copy_(master[k])
+            torch.cuda.synchronize()
+        with torch.no_grad():
+            return solver.solve(params, d["Q"], d["p"], d["A0"], d["zl"], d["zu"], mi, me, T, args.sigma,
+                                keep_unscaled=keep, packed=packed, timer=timer)
+
+    for _ in range(args.warmup):
+        step(None)
+    torch.cuda.synchronize()
+
+    timer = solver.Timer(True)
+    elapsed = 0.0
+    out = None
+    for _ in range(args.steps):
+        if dist:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        out = step(timer)
+        torch.cuda.synchronize()
+        elapsed += time.perf_counter() - t0
+    if dist:
+        t = torch.tensor([elapsed], device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t)
+    primal, dual = float(out["primal"].mean()), float(out["dual"].mean())
+
+    # dominant kernel and residual matvec, from the per-launch hipEvents of the timed steps
+    n_cell, ms_cell = timer.stats_ms("k:lstm_cell")
+    n_kkt, ms_kkt = timer.stats_ms("k:kkt_resgrad")
+    spans = timer.totals_ms()
+    cell_flop = B * (8.0 * N * h * h + 18.0 * N * h)            # per launch
+    kkt_bytes = B * (2.0 * (n * n + (mi + me) * n) * 4 + 10.0 * N * 4)
+    cell_tf = cell_flop / (ms_cell * 1e-3) / 1e12
+    kkt_gbs = kkt_bytes / (ms_kkt * 1e-3) / 1e9
+
+    res = None
+    if rank == 0:
+        total = world * B * args.steps
+        res = {
+            "metric": "QP instances/sec at n=1000 m=1000 K=100; final primal+dual residual",
+            "value": total / elapsed,
+            "unit": "QP instances/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": 1e3 * elapsed / args.steps,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic (generate_data.py:67-76 distribution, per-instance seeds; random-init weights)",
+            "config": {"workload": f"QP n={n} ineq={mi} eq={me} K={T} hidden={h} --test --scaling, "
+                                   f"batch={B}/GPU (BASELINE config {'2' if world == 1 else '3'})",
+                       "global_batch": world * B, "num_var": n, "num_ineq": mi, "num_eq": me,
+                       "outer_T": T, "hidden_dim": h, "parallelism": f"instance-shard x{world}",
+                       "in_place_scaling": not keep},
+            "final_residual": {"primal_mean": primal, "dual_mean": dual, "sum": primal + dual},
+            "roofline": {"kernel": "iadmm_lstm_cell_fwd", "bound": "mfma", "achieved": cell_tf,
+                         "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": cell_tf / FP32_MFMA_PEAK_TFLOPS,
+                         "traffic": None, "avg_launch_ms": ms_cell, "launches": n_cell,
+                         "algorithmic_per_launch": cell_flop},
+            "roofline_matvec": {"kernel": "iadmm_kkt_resgrad", "bound": "hbm", "achieved": kkt_gbs,
+                                "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": kkt_gbs / HBM_PEAK_GBS,
+                                "traffic": None, "avg_launch_ms": ms_kkt, "launches": n_kkt,
+                                "algorithmic_per_launch": kkt_bytes},
+            "phase_ms_per_step": {k: v / args.steps for k, v in spans.items() if not k.startswith("k:")},
+        }
+        if args.cpu_sample > 0:
+            res["cpu_baseline"] = cpu_baseline(args, d if keep else master, params)
+        print(json.dumps(res), flush=True)
+    if dist:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,361 @@
+// Implicit-KKT kernels: residual gradient g = K^T (K xv - b~), ||K xv - b~||, and the
+// primal/dual/objective metrics.  HBM-bound: each pass streams Q[n,n] and A0[m,n] of one
+// instance exactly once with 16-B coalesced loads; K itself is never formed.
+//
+// Reference: models/lstm.py:67-72 (K, b~, the two dependent bmm), main.py:952 (ls_res),
+// utils.py:53-54,68-71 (obj_fn, primal_dual_loss).
+#include "sweep.h"
+
+namespace iadmm {
+
+constexpr int kKktThreads = 256;
+
+struct KktArgs {
+  int n, m, num_ineq;
+  const float *Q, *A0, *p, *x, *y, *z, *xv;
+  float sigma;
+  const float* scal;
+  float *g, *btild, *rhovec, *lsres;
+};
+
+// One workgroup = one instance.  LDS: xs[n] (x~ -> r1), vs[m] (v -> r2), t1[n], t3[m], red[n].
+// PASS2=false stops after r and writes ||r||_2 (ls_res); PASS2=true computes g.
+template <int NG, bool VEC, bool PASS2>
+__global__ __launch_bounds__(kKktThreads) void kkt_kernel(KktArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  const int n = a.n, m = a.m, N = n + m;
+  float* xs = sm;
+  float* vs = xs + n;
+  float* t1 = vs + m;
+  float* t3 = t1 + n;
+  float* red = t3 + m;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, nw = blockDim.x >> 6;
+  const size_t b = blockIdx.x;
+  const float* Qb = a.Q + b * n * n;
+  const float* Ab = a.A0 + b * m * n;
+  const float* xvb = a.xv + b * N;
+  for (int i = tid; i < N; i += blockDim.x) {
+    if (i < n) xs[i] = xvb[i]; else vs[i - n] = xvb[i];
+  }
+  __syncthreads();
+
+  const float sigma = a.sigma;
+  const float rho_in = a.scal[IADMM_S_RHO_IN], rho_eq = a.scal[IADMM_S_RHO_EQ];
+  const float irho_in = a.scal[IADMM_S_IRHO_IN], irho_eq = a.scal[IADMM_S_IRHO_EQ];
+
+  // ---- pass 1: t1 = Q x~, t3 = A0 x~, red = A0^T v  (one read of Q and of A0)
+  float col[NG * 4];
+#pragma unroll
+  for (int i = 0; i < NG * 4; ++i) col[i] = 0.f;
+  sweep<NG, VEC, true, false>(Qb, n, n, xs, nullptr, t1, col, wave, nw, lane);
+  if (m > 0) sweep<NG, VEC, true, true>(Ab, m, n, xs, vs, t3, col, wave, nw, lane);
+  col_reduce<NG, VEC>(col, red, n, wave, nw, lane);
+
+  // ---- r = K xv - b~ (row i < n: (Q+sI) x~ + A0^T v - (s x - p); row n+j: A0 x~ - v/rho - (z - y/rho))
+  float ss = 0.f;
+  for (int i = tid; i < n; i += blockDim.x) {
+    const float b1 = sigma * a.x[b * n + i] - a.p[b * n + i];
+    const float r1 = ((t1[i] + sigma * xs[i]) + red[i]) - b1;
+    if (a.btild) a.btild[b * N + i] = b1;
+    if (PASS2) xs[i] = r1; else ss += r1 * r1;
+  }
+  for (int j = tid; j < m; j += blockDim.x) {
+    const bool ineq = j < a.num_ineq;
+    const float rho = ineq ? rho_in : rho_eq, irho = ineq ? irho_in : irho_eq;
+    const float b2 = a.z[b * m + j] - irho * a.y[b * m + j];
+    const float r2 = (t3[j] + (-irho) * vs[j]) - b2;
+    if (a.btild) a.btild[b * N + n + j] = b2;
+    if (a.rhovec) a.rhovec[b * m + j] = rho;
+    if (PASS2) vs[j] = r2; else ss += r2 * r2;
+  }
+  if constexpr (!PASS2) {
+    const float tot = block_sum(ss, red);
+    if (tid == 0) a.lsres[b] = sqrtf(tot);
+    return;
+  } else {
+    __syncthreads();
+    // ---- pass 2: red = Q^T r1 + A0^T r2 (one column accumulator), t3 = A0 r1
+#pragma unroll
+    for (int i = 0; i < NG * 4; ++i) col[i] = 0.f;
+    sweep<NG, VEC, false, true>(Qb, n, n, nullptr, xs, nullptr, col, wave, nw, lane);
+    if (m > 0) sweep<NG, VEC, true, true>(Ab, m, n, xs, vs, t3, col, wave, nw, lane);
+    col_reduce<NG, VEC>(col, red, n, wave, nw, lane);
+    for (int i = tid; i < n; i += blockDim.x) a.g[b * N + i] = red[i] + sigma * xs[i];
+    for (int j = tid; j < m; j += blockDim.x) {
+      const float irho = j < a.num_ineq ? irho_in : irho_eq;
+      a.g[b * N + n + j] = t3[j] + (-irho) * vs[j];
+    }
+  }
+}
+
+struct MetricArgs {
+  int n, m;
+  const float *Q, *p, *A0, *x, *y, *z;
+  float *obj, *primal, *dual;
+};
+
+// obj = 0.5 x^T(Qx) + p^T x ; primal = ||A0 x - z|| ; dual = ||(Qx + p) + A0^T y||
+template <int NG, bool VEC>
+__global__ __launch_bounds__(kKktThreads) void metrics_kernel(MetricArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  const int n = a.n, m = a.m;
+  float* xs = sm;
+  float* ys = xs + n;
+  float* t1 = ys + m;
+  float* t3 = t1 + n;
+  float* red = t3 + m;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, nw = blockDim.x >> 6;
+  const size_t b = blockIdx.x;
+  for (int i = tid; i < n; i += blockDim.x) xs[i] = a.x[b * n + i];
+  for (int j = tid; j < m; j += blockDim.x) ys[j] = a.y[b * m + j];
+  __syncthreads();
+  float col[NG * 4];
+#pragma unroll
+  for (int i = 0; i < NG * 4; ++i) col[i] = 0.f;
+  sweep<NG, VEC, true, false>(a.Q + b * n * n, n, n, xs, nullptr, t1, col, wave, nw, lane);
+  if (m > 0) sweep<NG, VEC, true, true>(a.A0 + b * m * n, m, n, xs, ys, t3, col, wave, nw, lane);
+  col_reduce<NG, VEC>(col, red, n, wave, nw, lane);
+  float xqx = 0.f, px = 0.f, dd = 0.f, pp = 0.f;
+  for (int i = tid; i < n; i += blockDim.x) {
+    const float pi = a.p[b * n + i];
+    xqx = fmaf(xs[i], t1[i], xqx);
+    px = fmaf(pi, xs[i], px);
+    const float d = (t1[i] + pi) + red[i];
+    dd = fmaf(d, d, dd);
+  }
+  for (int j = tid; j < m; j += blockDim.x) {
+    const float r = t3[j] - a.z[b * m + j];
+    pp = fmaf(r, r, pp);
+  }
+  // every block_sum is reached by all threads
+  const float s_xqx = block_sum(xqx, red);
+  const float s_px = block_sum(px, red);
+  const float s_dd = block_sum(dd, red);
+  const float s_pp = block_sum(pp, red);
+  if (tid == 0) {
+    if (a.obj) a.obj[b] = 0.5f * s_xqx + s_px;
+    if (a.primal) a.primal[b] = sqrtf(s_pp);
+    if (a.dual) a.dual[b] = sqrtf(s_dd);
+  }
+}
+
+__global__ void unscale_kernel(int64_t B, int n, int m, const float* D, const float* E,
+                               const float* c, const float* x, const float* y, const float* z,
+                               float* xo, float* yo, float* zo) {
+  const int64_t tot = B * (int64_t)(n + m);
+  for (int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; k < tot;
+       k += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t b = k / (n + m);
+    const int i = (int)(k - b * (n + m));
+    if (i < n) {
+      xo[b * n + i] = D[b * n + i] * x[b * n + i];
+    } else {
+      const int j = i - n;
+      const float e = E[b * m + j];
+      const float cinv = 1.0f / c[b];
+      yo[b * m + j] = (cinv * e) * y[b * m + j];   // bmm(cinv * E, y), main.py:1026
+      zo[b * m + j] = (1.0f / e) * z[b * m + j];   // bmm(Einv, z),      main.py:1027
+    }
+  }
+}
+
+// Batched matvec with a metric epilogue (utils.py:56-63 ineq_dist / eq_dist): one block per
+// instance, DOT sweep over rows.  mode 0: Mx x; 1: max(Mx x - rhs, 0); 2: |rhs - Mx x|.
+template <int NG, bool VEC>
+__global__ __launch_bounds__(kKktThreads) void bmv_kernel(int R, int C, const float* Mx,
+                                                           const float* x, const float* rhs,
+                                                           int mode, float* out) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  float* xs = sm;       // C
+  float* ds = xs + C;   // R
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, nw = blockDim.x >> 6;
+  const size_t b = blockIdx.x;
+  for (int i = tid; i < C; i += blockDim.x) xs[i] = x[b * C + i];
+  __syncthreads();
+  float col[NG * 4];
+  sweep<NG, VEC, true, false>(Mx + b * R * C, R, C, xs, nullptr, ds, col, wave, nw, lane);
+  __syncthreads();
+  for (int r = tid; r < R; r += blockDim.x) {
+    const float v = ds[r];
+    float o = v;
+    if (mode == 1) o = fmaxf(v - rhs[b * R + r], 0.f);
+    else if (mode == 2) o = fabsf(rhs[b * R + r] - v);
+    out[b * R + r] = o;
+  }
+}
+
+// Implicit K v (TRANS=false) or K^T v (TRANS=true): only the Q block differs.
+//   top = (Q or Q^T) v1 + sigma v1 + A0^T v2 ;  bottom = A0 v1 - v2 / rho
+template <int NG, bool VEC, bool TRANS>
+__global__ __launch_bounds__(kKktThreads) void kkt_matvec_kernel(KktArgs a, float* out) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  const int n = a.n, m = a.m, N = n + m;
+  float* xs = sm;
+  float* vs = xs + n;
+  float* t1 = vs + m;
+  float* t3 = t1 + n;
+  float* red = t3 + m;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, nw = blockDim.x >> 6;
+  const size_t b = blockIdx.x;
+  for (int i = tid; i < N; i += blockDim.x) {
+    if (i < n) xs[i] = a.xv[b * N + i]; else vs[i - n] = a.xv[b * N + i];
+  }
+  __syncthreads();
+  float col[NG * 4];
+#pragma unroll
+  for (int i = 0; i < NG * 4; ++i) col[i] = 0.f;
+  if constexpr (TRANS) sweep<NG, VEC, false, true>(a.Q + b * n * n, n, n, nullptr, xs, nullptr, col, wave, nw, lane);
+  else sweep<NG, VEC, true, false>(a.Q + b * n * n, n, n, xs, nullptr, t1, col, wave, nw, lane);
+  if (m > 0) sweep<NG, VEC, true, true>(a.A0 + b * m * n, m, n, xs, vs, t3, col, wave, nw, lane);
+  col_reduce<NG, VEC>(col, red, n, wave, nw, lane);
+  const float irho_in = a.scal[IADMM_S_IRHO_IN], irho_eq = a.scal[IADMM_S_IRHO_EQ];
+  for (int i = tid; i < n; i += blockDim.x) {
+    // TRANS: red already holds Q^T v1 + A0^T v2 (one column accumulator)
+    out[b * N + i] = TRANS ? red[i] + a.sigma * xs[i] : (t1[i] + a.sigma * xs[i]) + red[i];
+  }
+  for (int j = tid; j < m; j += blockDim.x) {
+    const float irho = j < a.num_ineq ? irho_in : irho_eq;
+    out[b * N + n + j] = t3[j] + (-irho) * vs[j];
+  }
+}
+
+// Dense K (models/lstm.py:67-68, models/lu.py:123-124) for Stage II and explicit inspection.
+__global__ void kkt_assemble_kernel(int64_t B, int n, int m, int num_ineq, const float* Q,
+                                    const float* A0, float sigma, const float* scal, float* K) {
+  const int N = n + m;
+  const int64_t tot = B * (int64_t)N * N;
+  const float irho_in = scal[IADMM_S_IRHO_IN], irho_eq = scal[IADMM_S_IRHO_EQ];
+  for (int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; k < tot;
+       k += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t b = k / ((int64_t)N * N);
+    const int rem = (int)(k - b * (int64_t)N * N);
+    const int i = rem / N, j = rem % N;
+    float v;
+    if (i < n && j < n) v = Q[(b * n + i) * n + j] + (i == j ? sigma : 0.f);
+    else if (i < n) v = A0[(b * m + (j - n)) * n + i];
+    else if (j < n) v = A0[(b * m + (i - n)) * n + j];
+    else v = (i == j) ? -((i - n) < num_ineq ? irho_in : irho_eq) : -0.f;
+    K[k] = v;
+  }
+}
+
+inline bool kkt_fits(int64_t n, int64_t m) { return 3 * n + 2 * m <= 40960; }
+
+template <bool PASS2>
+int launch_kkt(int64_t B, int64_t n, int64_t m, KktArgs a, hipStream_t s) {
+  const int ng = ng_for(n);
+  const bool vec = (n % 4 == 0) && aligned16(a.Q) && (m == 0 || aligned16(a.A0));
+  const size_t lds = (3 * n + 2 * m) * sizeof(float);
+  IADMM_DISPATCH_NG(ng, vec, {
+    hipLaunchKernelGGL((kkt_kernel<NG_, V_, PASS2>), dim3((unsigned)B), dim3(kKktThreads), lds, s, a);
+  });
+  IADMM_CHECK_LAUNCH();
+  return 0;
+}
+
+}  // namespace iadmm
+
+using namespace iadmm;
+
+extern "C" int iadmm_kkt_resgrad(int64_t B, int64_t n, int64_t m, int64_t num_ineq,
+                                 const float* Q, const float* A0, const float* p, const float* x,
+                                 const float* y, const float* z, const float* xv, float sigma,
+                                 const float* scal, float* g, float* btild, float* rho_vec,
+                                 void* stream) {
+  if (B <= 0 || n <= 0 || m < 0 || num_ineq < 0 || num_ineq > m) return IADMM_E_ARG;
+  if (!Q || !p || !x || !xv || !scal || !g || (m > 0 && (!A0 || !y || !z))) return IADMM_E_ARG;
+  if (!kkt_fits(n, m) || B > 0x7fffffff) return IADMM_E_SIZE;
+  KktArgs a{(int)n, (int)m, (int)num_ineq, Q, A0, p, x, y, z, xv, sigma, scal, g, btild, rho_vec, nullptr};
+  return launch_kkt<true>(B, n, m, a, (hipStream_t)stream);
+}
+
+extern "C" int iadmm_kkt_lsres(int64_t B, int64_t n, int64_t m, int64_t num_ineq,
+                               const float* Q, const float* A0, const float* p, const float* x,
+                               const float* y, const float* z, const float* xv, float sigma,
+                               const float* scal, float* out, void* stream) {
+  if (B <= 0 || n <= 0 || m < 0 || num_ineq < 0 || num_ineq > m) return IADMM_E_ARG;
+  if (!Q || !p || !x || !xv || !scal || !out || (m > 0 && (!A0 || !y || !z))) return IADMM_E_ARG;
+  if (!kkt_fits(n, m) || B > 0x7fffffff) return IADMM_E_SIZE;
+  KktArgs a{(int)n, (int)m, (int)num_ineq, Q, A0, p, x, y, z, xv, sigma, scal, nullptr, nullptr, nullptr, out};
+  return launch_kkt<false>(B, n, m, a, (hipStream_t)stream);
+}
+
+extern "C" int iadmm_metrics(int64_t B, int64_t n, int64_t m, const float* Q, const float* p,
+                             const float* A0, const float* x, const float* y, const float* z,
+                             float* obj, float* primal, float* dual, void* stream) {
+  if (B <= 0 || n <= 0 || m < 0 || !Q || !p || !x || (m > 0 && (!A0 || !y || !z))) return IADMM_E_ARG;
+  if (!kkt_fits(n, m) || B > 0x7fffffff) return IADMM_E_SIZE;
+  MetricArgs a{(int)n, (int)m, Q, p, A0, x, y, z, obj, primal, dual};
+  const int ng = ng_for(n);
+  const bool vec = (n % 4 == 0) && aligned16(Q) && (m == 0 || aligned16(A0));
+  const size_t lds = (3 * n + 2 * m) * sizeof(float);
+  IADMM_DISPATCH_NG(ng, vec, {
+    hipLaunchKernelGGL((metrics_kernel<NG_, V_>), dim3((unsigned)B), dim3(kKktThreads), lds,
+                       (hipStream_t)stream, a);
+  });
+  IADMM_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int iadmm_unscale(int64_t B, int64_t n, int64_t m, const float* D, const float* E,
+                             const float* c, const float* x, const float* y, const float* z,
+                             float* x_out, float* y_out, float* z_out, void* stream) {
+  if (B <= 0 || n <= 0 || m < 0 || !D || !c || !x || !x_out) return IADMM_E_ARG;
+  if (m > 0 && (!E || !y || !z || !y_out || !z_out)) return IADMM_E_ARG;
+  const int64_t tot = B * (n + m);
+  const unsigned grid = (unsigned)((tot + 255) / 256 < 65536 ? (tot + 255) / 256 : 65536);
+  hipLaunchKernelGGL(unscale_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, B, (int)n,
+                     (int)m, D, E, c, x, y, z, x_out, y_out, z_out);
+  IADMM_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int iadmm_bmv(int64_t B, int64_t R, int64_t C, const float* Mx, const float* x,
+                         const float* rhs, int mode, float* out, void* stream) {
+  if (B <= 0 || R <= 0 || C <= 0 || !Mx || !x || !out || mode < 0 || mode > 2) return IADMM_E_ARG;
+  if (mode != 0 && !rhs) return IADMM_E_ARG;
+  if (R + C > 40960 || B > 0x7fffffff) return IADMM_E_SIZE;
+  const int ng = ng_for(C);
+  const bool vec = (C % 4 == 0) && aligned16(Mx);
+  const size_t lds = (R + C) * sizeof(float);
+  IADMM_DISPATCH_NG(ng, vec, {
+    hipLaunchKernelGGL((bmv_kernel<NG_, V_>), dim3((unsigned)B), dim3(kKktThreads), lds,
+                       (hipStream_t)stream, (int)R, (int)C, Mx, x, rhs, mode, out);
+  });
+  IADMM_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int iadmm_kkt_matvec(int64_t B, int64_t n, int64_t m, int64_t num_ineq, const float* Q,
+                                const float* A0, const float* v, float sigma, const float* scal,
+                                int transpose, float* out, void* stream) {
+  if (B <= 0 || n <= 0 || m < 0 || num_ineq < 0 || num_ineq > m) return IADMM_E_ARG;
+  if (!Q || !v || !scal || !out || (m > 0 && !A0)) return IADMM_E_ARG;
+  if (!kkt_fits(n, m) || B > 0x7fffffff) return IADMM_E_SIZE;
+  KktArgs a{(int)n, (int)m, (int)num_ineq, Q, A0, nullptr, nullptr, nullptr, nullptr, v, sigma, scal,
+            nullptr, nullptr, nullptr, nullptr};
+  const int ng = ng_for(n);
+  const bool vec = (n % 4 == 0) && aligned16(Q) && (m == 0 || aligned16(A0));
+  const size_t lds = (3 * n + 2 * m) * sizeof(float);
+  hipStream_t s = (hipStream_t)stream;
+  if (transpose) {
+    IADMM_DISPATCH_NG(ng, vec, { hipLaunchKernelGGL((kkt_matvec_kernel<NG_, V_, true>), dim3((unsigned)B), dim3(kKktThreads), lds, s, a, out); });
+  } else {
+    IADMM_DISPATCH_NG(ng, vec, { hipLaunchKernelGGL((kkt_matvec_kernel<NG_, V_, false>), dim3((unsigned)B), dim3(kKktThreads), lds, s, a, out); });
+  }
+  IADMM_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int iadmm_kkt_assemble(int64_t B, int64_t n, int64_t m, int64_t num_ineq, const float* Q,
+                                  const float* A0, float sigma, const float* scal, float* K,
+                                  void* stream) {
+  if (B <= 0 || n <= 0 || m < 0 || num_ineq < 0 || num_ineq > m || !Q || !scal || !K || (m > 0 && !A0))
+    return IADMM_E_ARG;
+  const int64_t tot = B * (n + m) * (n + m);
+  const int64_t blocks = (tot + 255) / 256;
+  hipLaunchKernelGGL(kkt_assemble_kernel, dim3((unsigned)(blocks < 16384 ? blocks : 16384)), dim3(256), 0,
+                     (hipStream_t)stream, B, (int)n, (int)m, (int)num_ineq, Q, A0, sigma, scal, K);
+  IADMM_CHECK_LAUNCH();
+  return 0;
+}

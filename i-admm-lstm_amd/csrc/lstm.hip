@@ -1,0 +1,281 @@
+// Fused coordinate-wise LSTM cell on fp32 MFMA (gfx950 v_mfma_f32_32x32x2_f32).
+//
+// Reference: models/lstm.py:74-80.  For every row r of the M = B*(n+m) coordinate rows and every
+// hidden unit j:
+//   pre_g[r,j] = (in0[r] W_g[0,j] + in1[r] W_g[1,j]) + sum_k H[r,k] U_g[k,j] + b_g[j]
+//   I,F,O = sigmoid(pre_{i,f,o}), U = tanh(pre_u), C' = I U + F C, H' = O tanh(C')
+//   part[tile(j)][r] += H'[r,j] W_h[j]      (the output projection, reduced per 32-unit tile)
+//
+// GEMM shape: rows M (2.048M at the bench config) x 4h gate columns x K = h.  The weights are the
+// MFMA "A" operand (M-dim of the instruction = hidden unit), H is the "B" operand (N-dim = data
+// row), so the accumulator of one wave holds, for its 64 data rows and 32 hidden units, all FOUR
+// gates at the same register index: the whole cell update runs in registers in the epilogue.
+//
+// Tile: workgroup = 4 waves = 32 hidden units x 256 rows; wave = 32 hidden x 64 rows x 4 gates
+// (8 accumulators of 32x32 = 128 acc registers).  K is staged in chunks of 32 through padded LDS
+// (row stride 36 floats: conflict-free ds_read_b128 for 16 distinct rows), with the next chunk
+// prefetched into registers while the MFMAs run.  Workgroups are remapped XCD-aware so the njt
+// hidden tiles of one 256-row H panel run back to back on the same XCD (panel read from HBM once,
+// then served by that XCD's L2).
+#include "common.h"
+
+namespace iadmm {
+
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+
+constexpr int kJT = 32;          // hidden units per workgroup
+constexpr int kRows = 256;       // data rows per workgroup
+constexpr int kBK = 32;          // K chunk
+constexpr int kLD = kBK + 4;     // padded LDS row (floats)
+constexpr int kWxF = 16;         // packed per-unit fields: Wi0 Wi1 bi Wf0 Wf1 bf Wo0 Wo1 bo Wu0 Wu1 bu Wh
+
+inline int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
+
+// Upk[((jt*nkc + kc)*128 + g*32 + jj)*32 + kk] = U_g[kc*32 + kk][jt*32 + jj]  (0 outside h)
+__global__ void lstm_pack_kernel(int h, int njt, int nkc, const float* U0, const float* U1,
+                                 const float* U2, const float* U3, float* Upk) {
+  const int64_t tot = (int64_t)njt * nkc * 128 * kBK;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < tot;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int kk = (int)(i % kBK);
+    int64_t t = i / kBK;
+    const int row = (int)(t % 128);
+    t /= 128;
+    const int kc = (int)(t % nkc);
+    const int jt = (int)(t / nkc);
+    const int g = row >> 5, jj = row & 31;
+    const int k = kc * kBK + kk, j = jt * kJT + jj;
+    const float* U = g == 0 ? U0 : (g == 1 ? U1 : (g == 2 ? U2 : U3));
+    Upk[i] = (k < h && j < h) ? U[(int64_t)k * h + j] : 0.f;
+  }
+}
+
+struct WxSrc { const float *W[4], *b[4], *Wh; };
+
+__global__ void lstm_pack_wx_kernel(int h, int hp, WxSrc s, float* Wx) {
+  const int tot = hp * kWxF;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < tot; i += gridDim.x * blockDim.x) {
+    const int j = i / kWxF, f = i % kWxF;
+    float v = 0.f;
+    if (j < h) {
+      if (f < 12) {
+        const int g = f / 3, w = f % 3;
+        v = w < 2 ? s.W[g][(int64_t)w * h + j] : s.b[g][j];
+      } else if (f == 12) {
+        v = s.Wh[j];
+      }
+    }
+    Wx[i] = v;
+  }
+}
+
+struct CellArgs {
+  int64_t M;
+  int h, njt, nkc, nrt;
+  const float *H, *C, *xv, *g, *Upk, *Wx;
+  float *Hn, *Cn, *part;
+};
+
+template <bool VEC>
+__global__ __launch_bounds__(256, 2) void lstm_cell_kernel(CellArgs a) {
+  __shared__ __attribute__((aligned(16))) float sA[128 * kLD];
+  __shared__ __attribute__((aligned(16))) float sB[kRows * kLD];
+  __shared__ __attribute__((aligned(16))) float sW[kWxF * kJT];
+
+  // XCD-aware bijective remap: blocks b, b+8, ... share an XCD; give each XCD a contiguous run
+  // of logical tiles with the hidden tile fastest, so an H panel is reused from that XCD's L2.
+  const int nwg = gridDim.x, bid = blockIdx.x;
+  const int xcd = bid & 7, local = bid >> 3, q8 = nwg >> 3, r8 = nwg & 7;
+  const int logical = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + local;
+  const int jt = logical % a.njt;
+  const int rt = logical / a.njt;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int jl = lane & 31, hf = lane >> 5;
+  const int h = a.h;
+  const int64_t M = a.M;
+  const int64_t rbase = (int64_t)rt * kRows;
+
+  for (int i = tid; i < kWxF * kJT; i += 256) {
+    const int f = i / kJT, jj = i % kJT;
+    sW[i] = a.Wx[(int64_t)(jt * kJT + jj) * kWxF + f];
+  }
+
+  floatx16 acc[4][2];
+#pragma unroll
+  for (int g = 0; g < 4; ++g)
+#pragma unroll
+    for (int r = 0; r < 2; ++r)
+#pragma unroll
+      for (int q = 0; q < 16; ++q) acc[g][r][q] = 0.f;
+
+  float4 ra[4], rb[8];
+  const float* Ubase = a.Upk + (int64_t)jt * a.nkc * 128 * kBK;
+  auto gload = [&](int kc) {
+    const float4* Ac = reinterpret_cast<const float4*>(Ubase + (int64_t)kc * 128 * kBK);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) ra[i] = Ac[tid + 256 * i];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int idx = tid + 256 * i, row = idx >> 3, c4 = idx & 7;
+      const int64_t R = rbase + row;
+      const int k = kc * kBK + c4 * 4;
+      if constexpr (VEC) {
+        rb[i] = (R < M && k < h) ? *reinterpret_cast<const float4*>(a.H + R * h + k)
+                                 : make_float4(0.f, 0.f, 0.f, 0.f);
+      } else {
+        float4 t;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) set4(t, e, (R < M && k + e < h) ? a.H[R * h + k + e] : 0.f);
+        rb[i] = t;
+      }
+    }
+  };
+
+  gload(0);
+  for (int kc = 0; kc < a.nkc; ++kc) {
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int idx = tid + 256 * i, row = idx >> 3, c4 = idx & 7;
+      *reinterpret_cast<float4*>(&sA[row * kLD + c4 * 4]) = ra[i];
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int idx = tid + 256 * i, row = idx >> 3, c4 = idx & 7;
+      *reinterpret_cast<float4*>(&sB[row * kLD + c4 * 4]) = rb[i];
+    }
+    __syncthreads();
+    if (kc + 1 < a.nkc) gload(kc + 1);
+#pragma unroll
+    for (int G = 0; G < kBK / 8; ++G) {
+      float4 af[4], bf[2];
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+        af[g] = *reinterpret_cast<const float4*>(&sA[(g * 32 + jl) * kLD + 8 * G + 4 * hf]);
+#pragma unroll
+      for (int r = 0; r < 2; ++r)
+        bf[r] = *reinterpret_cast<const float4*>(&sB[(wave * 64 + r * 32 + jl) * kLD + 8 * G + 4 * hf]);
+#pragma unroll
+      for (int s = 0; s < 4; ++s)
+#pragma unroll
+        for (int g = 0; g < 4; ++g)
+#pragma unroll
+          for (int r = 0; r < 2; ++r)
+            acc[g][r] = __builtin_amdgcn_mfma_f32_32x32x2f32(get4(af[g], s), get4(bf[r], s),
+                                                             acc[g][r], 0, 0, 0);
+    }
+  }
+
+  // ---- epilogue: gates, cell update, projection partial (all in registers)
+  // accumulator element q of lane (jl,hf): hidden jj = (q&3) + 8*(q>>2) + 4*hf, data row jl.
+#pragma unroll
+  for (int r = 0; r < 2; ++r) {
+    const int64_t R = rbase + wave * 64 + r * 32 + jl;
+    const bool rok = R < M;
+    const float in0 = rok ? a.xv[R] : 0.f;
+    const float in1 = rok ? a.g[R] : 0.f;
+    float gsum = 0.f;
+#pragma unroll
+    for (int qq = 0; qq < 4; ++qq) {
+      const int jj0 = 8 * qq + 4 * hf;
+      const int j0 = jt * kJT + jj0;
+      float4 cold;
+      if constexpr (VEC) {
+        cold = (rok && j0 < h) ? *reinterpret_cast<const float4*>(a.C + R * h + j0)
+                               : make_float4(0.f, 0.f, 0.f, 0.f);
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) set4(cold, e, (rok && j0 + e < h) ? a.C[R * h + j0 + e] : 0.f);
+      }
+      float4 wv[13];
+#pragma unroll
+      for (int f = 0; f < 13; ++f) wv[f] = *reinterpret_cast<const float4*>(&sW[f * kJT + jj0]);
+      float4 cnew, hnew;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int q = qq * 4 + e;
+        float pre[4];
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const float xw = in0 * get4(wv[3 * g], e) + in1 * get4(wv[3 * g + 1], e);
+          pre[g] = (xw + acc[g][r][q]) + get4(wv[3 * g + 2], e);
+        }
+        const float ig = sigmoidf_(pre[0]), fg = sigmoidf_(pre[1]), og = sigmoidf_(pre[2]);
+        const float ug = tanhf(pre[3]);
+        const float c2 = ig * ug + fg * get4(cold, e);
+        const float h2 = og * tanhf(c2);
+        set4(cnew, e, c2);
+        set4(hnew, e, h2);
+        gsum = fmaf(h2, get4(wv[12], e), gsum);
+      }
+      if (rok) {
+        if constexpr (VEC) {
+          if (j0 < h) {
+            *reinterpret_cast<float4*>(a.Cn + R * h + j0) = cnew;
+            *reinterpret_cast<float4*>(a.Hn + R * h + j0) = hnew;
+          }
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            if (j0 + e < h) {
+              a.Cn[R * h + j0 + e] = get4(cnew, e);
+              a.Hn[R * h + j0 + e] = get4(hnew, e);
+            }
+          }
+        }
+      }
+    }
+    gsum += __shfl_xor(gsum, 32, 64);
+    if (hf == 0 && rok) a.part[(int64_t)jt * M + R] = gsum;
+  }
+}
+
+}  // namespace iadmm
+
+using namespace iadmm;
+
+extern "C" int64_t iadmm_lstm_ntiles(int64_t h) { return cdiv(h, kJT); }
+extern "C" int64_t iadmm_lstm_packed_floats(int64_t h) { return cdiv(h, kJT) * cdiv(h, kBK) * 128 * kBK; }
+extern "C" int64_t iadmm_lstm_wx_floats(int64_t h) { return cdiv(h, kJT) * kJT * kWxF; }
+
+extern "C" int iadmm_lstm_pack(int64_t h, const float* W_i, const float* U_i, const float* b_i,
+                               const float* W_f, const float* U_f, const float* b_f,
+                               const float* W_o, const float* U_o, const float* b_o,
+                               const float* W_u, const float* U_u, const float* b_u,
+                               const float* W_h, float* Upk, float* Wx, void* stream) {
+  if (h <= 0 || h > (1 << 20)) return IADMM_E_ARG;
+  const float* ptrs[] = {W_i, U_i, b_i, W_f, U_f, b_f, W_o, U_o, b_o, W_u, U_u, b_u, W_h, Upk, Wx};
+  for (const float* p : ptrs)
+    if (!p) return IADMM_E_ARG;
+  if (!aligned16(Upk)) return IADMM_E_ALIGN;
+  const int njt = (int)cdiv(h, kJT), nkc = (int)cdiv(h, kBK);
+  hipStream_t s = (hipStream_t)stream;
+  hipLaunchKernelGGL(lstm_pack_kernel, dim3(2048), dim3(256), 0, s, (int)h, njt, nkc, U_i, U_f,
+                     U_o, U_u, Upk);
+  IADMM_CHECK_LAUNCH();
+  WxSrc src{{W_i, W_f, W_o, W_u}, {b_i, b_f, b_o, b_u}, W_h};
+  hipLaunchKernelGGL(lstm_pack_wx_kernel, dim3(64), dim3(256), 0, s, (int)h, njt * kJT, src, Wx);
+  IADMM_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int iadmm_lstm_cell_fwd(int64_t M, int64_t h, const float* H, const float* C,
+                                   const float* xv, const float* g, const float* Upk,
+                                   const float* Wx, float* Hn, float* Cn, float* part,
+                                   void* stream) {
+  if (M <= 0 || h <= 0 || !H || !C || !xv || !g || !Upk || !Wx || !Hn || !Cn || !part) return IADMM_E_ARG;
+  if (Hn == H) return IADMM_E_ARG;  // other workgroups still read H rows
+  if (!aligned16(Upk)) return IADMM_E_ALIGN;
+  const int64_t nrt = cdiv(M, kRows), njt = cdiv(h, kJT);
+  if (nrt * njt > 0x7fffffffLL || h > (1 << 16)) return IADMM_E_SIZE;
+  CellArgs a{M, (int)h, (int)njt, (int)cdiv(h, kBK), (int)nrt, H, C, xv, g, Upk, Wx, Hn, Cn, part};
+  const bool vec = (h % 4 == 0) && aligned16(H) && aligned16(C) && aligned16(Hn) && aligned16(Cn);
+  const dim3 grid((unsigned)(nrt * njt));
+  if (vec)
+    hipLaunchKernelGGL(lstm_cell_kernel<true>, grid, dim3(256), 0, (hipStream_t)stream, a);
+  else
+    hipLaunchKernelGGL(lstm_cell_kernel<false>, grid, dim3(256), 0, (hipStream_t)stream, a);
+  IADMM_CHECK_LAUNCH();
+  return 0;
+}

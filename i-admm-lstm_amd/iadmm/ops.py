@@ -1,0 +1,187 @@
+"""Tensor-level wrappers around the C-ABI (one function per kernel family).
+
+Every wrapper takes contiguous fp32 tensors on the current HIP device, allocates its outputs
+with the PyTorch caching allocator, launches on the current stream and returns.  There is no
+host synchronisation and no CPU path: a CPU tensor or a missing library raises.
+"""
+from __future__ import annotations
+
+import torch
+
+from . import _abi
+
+NSCAL = 8  # IADMM_NSCAL
+S_RHO_IN, S_RHO_EQ, S_IRHO_IN, S_IRHO_EQ, S_ALPHA, S_1MALPHA = range(6)
+
+
+def _stream():
+    return torch.cuda.current_stream().cuda_stream
+
+
+def _p(t):
+    """Device pointer of a contiguous fp32 device tensor (None -> NULL)."""
+    if t is None:
+        return None
+    if not t.is_cuda:
+        raise ValueError("iadmm kernels need device tensors (no CPU fallback)")
+    if t.dtype != torch.float32:
+        raise TypeError(f"iadmm kernels compute in fp32, got {t.dtype}")
+    if not t.is_contiguous():
+        raise ValueError("iadmm kernels need contiguous tensors")
+    return t.data_ptr()
+
+
+def _c(t):
+    return None if t is None else t.detach().float().contiguous()
+
+
+def empty(*shape, like):
+    return torch.empty(*shape, dtype=torch.float32, device=like.device)
+
+
+# --------------------------------------------------------------------------- schedule
+def schedule(rho_param, alpha_param, t, out=None):
+    """Iteration scalars of step t (models/lstm.py:60-63) into a device [8] buffer."""
+    out = empty(NSCAL, like=rho_param) if out is None else out
+    _abi.call("iadmm_schedule", _p(rho_param), _p(alpha_param), int(t), _p(out), _stream())
+    return out
+
+
+def schedule_fixed_alpha(scal, alpha, out=None):
+    out = torch.empty_like(scal) if out is None else out
+    _abi.call("iadmm_schedule_fixed_alpha", _p(scal), float(alpha), _p(out), _stream())
+    return out
+
+
+# --------------------------------------------------------------------------- KKT
+def kkt_resgrad(Q, A0, p, x, y, z, xv, sigma, scal, num_ineq, g=None, btild=None, rho_vec=None):
+    """g = K^T (K xv - b~) with the implicit KKT matrix (models/lstm.py:67-72)."""
+    B, n = Q.shape[0], Q.shape[1]
+    m = A0.shape[1]
+    g = empty(B, n + m, like=Q) if g is None else g
+    _abi.call("iadmm_kkt_resgrad", B, n, m, int(num_ineq), _p(Q), _p(A0), _p(p), _p(x), _p(y), _p(z),
+              _p(xv), float(sigma), _p(scal), _p(g), _p(btild), _p(rho_vec), _stream())
+    return g
+
+
+def kkt_lsres(Q, A0, p, x, y, z, xv, sigma, scal, num_ineq, out=None):
+    """Per-instance ||K xv - b~||_2 (main.py:952)."""
+    B, n = Q.shape[0], Q.shape[1]
+    m = A0.shape[1]
+    out = empty(B, like=Q) if out is None else out
+    _abi.call("iadmm_kkt_lsres", B, n, m, int(num_ineq), _p(Q), _p(A0), _p(p), _p(x), _p(y), _p(z),
+              _p(xv), float(sigma), _p(scal), _p(out), _stream())
+    return out
+
+
+# --------------------------------------------------------------------------- LSTM cell
+def lstm_ntiles(h):
+    return int(_abi.lib().iadmm_lstm_ntiles(int(h)))
+
+
+def lstm_pack(params, h):
+    """Pack W_*, U_*, b_*, W_h (models/lstm.py:21-38) into the cell kernel's layout."""
+    L = _abi.lib()
+    ref = params["U_i"]
+    Upk = empty(int(L.iadmm_lstm_packed_floats(h)), like=ref)
+    Wx = empty(int(L.iadmm_lstm_wx_floats(h)), like=ref)
+    ps = [_c(params[k]) for k in ("W_i", "U_i", "b_i", "W_f", "U_f", "b_f", "W_o", "U_o", "b_o",
+                                  "W_u", "U_u", "b_u", "W_h")]
+    _abi.call("iadmm_lstm_pack", int(h), *[_p(t) for t in ps], _p(Upk), _p(Wx), _stream())
+    return Upk, Wx
+
+
+def lstm_cell(H, C, xv, g, Upk, Wx, Hn=None, Cn=None, part=None):
+    """Fused LSTM cell over M rows; returns (Hn, Cn, part[ntiles, M]).  Cn may alias C."""
+    h = H.shape[-1]
+    M = H.numel() // h
+    Hn = torch.empty_like(H) if Hn is None else Hn
+    Cn = torch.empty_like(C) if Cn is None else Cn
+    part = empty(lstm_ntiles(h), M, like=H) if part is None else part
+    _abi.call("iadmm_lstm_cell_fwd", M, h, _p(H), _p(C), _p(xv), _p(g), _p(Upk), _p(Wx), _p(Hn), _p(Cn),
+              _p(part), _stream())
+    return Hn, Cn, part
+
+
+# --------------------------------------------------------------------------- ADMM update
+def admm_update(n, m, num_ineq, part, b_h, xv, x, y, z, zl, zu, scal, relax_z=False, out=None,
+                rho_vec=None):
+    """xv' / x' / z' / y' (models/lstm.py:80-94; relax_z -> models/lu.py:133-140)."""
+    B = x.shape[0]
+    if out is None:
+        out = (torch.empty_like(xv), torch.empty_like(x), torch.empty_like(y), torch.empty_like(z))
+    xvo, xo, yo, zo = out
+    ntiles = 0 if part is None else part.shape[0]
+    _abi.call("iadmm_admm_update", B, n, m, int(num_ineq), ntiles, _p(part), _p(b_h), _p(xv), _p(x), _p(y),
+              _p(z), _p(zl), _p(zu), _p(scal), int(bool(relax_z)), _p(xvo), _p(xo), _p(yo), _p(zo),
+              _p(rho_vec), _stream())
+    return xvo, xo, yo, zo
+
+
+# --------------------------------------------------------------------------- Ruiz / unscale / metrics
+def ruiz_scale(Q, p, A0, zl, zu, iters=10, out=None):
+    """Modified Ruiz + cost scaling (methods/scaling.py:50-119).  Returns
+    (Q, p, A0, zl, zu, D[B,n], E[B,m], c[B]).  ``out`` may be the inputs (in place)."""
+    B, n = Q.shape[0], Q.shape[1]
+    m = A0.shape[1]
+    if out is None:
+        out = (torch.empty_like(Q), torch.empty_like(p), torch.empty_like(A0), torch.empty_like(zl),
+               torch.empty_like(zu))
+    Qo, po, Ao, zlo, zuo = out
+    D, E, c = empty(B, n, like=Q), empty(B, m, like=Q), empty(B, like=Q)
+    _abi.call("iadmm_ruiz_scale", B, n, m, int(iters), _p(Q), _p(p), _p(A0), _p(zl), _p(zu), _p(Qo), _p(po),
+              _p(Ao), _p(zlo), _p(zuo), _p(D), _p(E), _p(c), _stream())
+    return Qo, po, Ao, zlo, zuo, D, E, c
+
+
+def unscale(D, E, c, x, y, z, out=None):
+    """x = D x, y = (c^-1 E) y, z = E^-1 z (main.py:1025-1027)."""
+    B, n = x.shape[0], x.shape[1]
+    m = y.shape[1]
+    if out is None:
+        out = (torch.empty_like(x), torch.empty_like(y), torch.empty_like(z))
+    xo, yo, zo = out
+    _abi.call("iadmm_unscale", B, n, m, _p(D), _p(E), _p(c), _p(x), _p(y), _p(z), _p(xo), _p(yo), _p(zo),
+              _stream())
+    return xo, yo, zo
+
+
+def metrics(Q, p, A0, x, y, z):
+    """(obj, primal, dual) per instance, each [B] (utils.py:53-54, 68-71)."""
+    B, n = Q.shape[0], Q.shape[1]
+    m = A0.shape[1]
+    obj, pr, du = empty(B, like=Q), empty(B, like=Q), empty(B, like=Q)
+    _abi.call("iadmm_metrics", B, n, m, _p(Q), _p(p), _p(A0), _p(x), _p(y), _p(z), _p(obj), _p(pr), _p(du),
+              _stream())
+    return obj, pr, du
+
+
+BMV_PLAIN, BMV_POS_EXCESS, BMV_ABS_GAP = 0, 1, 2
+
+
+def bmv(Mx, x, rhs=None, mode=BMV_PLAIN):
+    """Batched matvec with a fused metric epilogue: Mx x, clamp(Mx x - rhs, 0) or |rhs - Mx x|."""
+    B, R, C = Mx.shape
+    out = empty(B, R, like=Mx)
+    _abi.call("iadmm_bmv", B, R, C, _p(Mx), _p(x), _p(rhs), int(mode), _p(out), _stream())
+    return out
+
+
+def kkt_matvec(Q, A0, v, sigma, scal, num_ineq, transpose=False):
+    """Implicit K v or K^T v, v[B,n+m] -> [B,n+m]."""
+    B, n = Q.shape[0], Q.shape[1]
+    m = A0.shape[1]
+    out = empty(B, n + m, like=Q)
+    _abi.call("iadmm_kkt_matvec", B, n, m, int(num_ineq), _p(Q), _p(A0), _p(v), float(sigma), _p(scal),
+              int(bool(transpose)), _p(out), _stream())
+    return out
+
+
+def kkt_assemble(Q, A0, sigma, scal, num_ineq):
+    """Dense K[B,n+m,n+m]."""
+    B, n = Q.shape[0], Q.shape[1]
+    m = A0.shape[1]
+    K = empty(B, n + m, n + m, like=Q)
+    _abi.call("iadmm_kkt_assemble", B, n, m, int(num_ineq), _p(Q), _p(A0), float(sigma), _p(scal), _p(K),
+              _stream())
+    return K

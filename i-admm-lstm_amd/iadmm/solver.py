@@ -1,0 +1,197 @@
+"""Fused test-mode solve loop (the hot path of main.py --test, main.py:818-1031).
+
+One call = Ruiz scaling -> T Stage-I iterations -> final unscale -> final metrics, for one batch
+of instances that is already resident in HBM.  Every step is a HIP kernel from libiadmm.so on
+the current stream; no host synchronisation happens inside (metrics are kept on the device and
+copied once at the end when ``history`` is requested).
+
+Per iteration t (4 launches):
+  iadmm_schedule      rho/alpha scalars of step t            models/lstm.py:60-63
+  iadmm_kkt_resgrad   g = K^T (K xv - b~), implicit K        models/lstm.py:67-72
+  iadmm_lstm_cell_fwd gates on fp32 MFMA + cell + projection models/lstm.py:74-80
+  iadmm_admm_update   xv, x, z, y updates                    models/lstm.py:80-94
+Buffers: x/y/z/xv and H ping-pong between two sets owned by the solver; C is updated in place.
+"""
+from __future__ import annotations
+
+import torch
+
+from . import ops
+
+PARAM_NAMES = tuple(f"{a}_{g}" for g in "ifou" for a in ("W", "U", "b")) + ("W_h", "b_h", "rho", "alpha")
+
+
+def param_dict(model_or_dict):
+    if isinstance(model_or_dict, dict):
+        return {k: model_or_dict[k] for k in PARAM_NAMES}
+    return {k: getattr(model_or_dict, k) for k in PARAM_NAMES}
+
+
+class PackedWeights:
+    """Cell-kernel weight layout, re-packed only when a parameter changes (in-place updates bump
+    ``_version``; replacing a tensor changes its data_ptr)."""
+
+    def __init__(self):
+        self._key = None
+        self.Upk = self.Wx = None
+
+    def get(self, params, h):
+        key = tuple((params[k].data_ptr(), params[k]._version) for k in PARAM_NAMES[:13]) + (h,)
+        if key != self._key:
+            with torch.no_grad():
+                self.Upk, self.Wx = ops.lstm_pack(params, h)
+            self._key = key
+        return self.Upk, self.Wx
+
+
+class Timer:
+    """hipEvent brackets on the current stream (named spans, summed)."""
+
+    def __init__(self, enabled):
+        self.enabled = enabled
+        self.spans = {}
+
+    def start(self, name):
+        if not self.enabled:
+            return None
+        ev = torch.cuda.Event(enable_timing=True)
+        ev.record()
+        return (name, ev)
+
+    def stop(self, tok):
+        if tok is None:
+            return
+        ev = torch.cuda.Event(enable_timing=True)
+        ev.record()
+        self.spans.setdefault(tok[0], []).append((tok[1], ev))
+
+    def totals_ms(self):
+        torch.cuda.synchronize()
+        return {k: sum(a.elapsed_time(b) for a, b in v) for k, v in self.spans.items()}
+
+    def stats_ms(self, name):
+        """(count, mean ms) of one span name."""
+        torch.cuda.synchronize()
+        v = self.spans.get(name, [])
+        if not v:
+            return 0, float("nan")
+        return len(v), sum(a.elapsed_time(b) for a, b in v) / len(v)
+
+    def reset(self):
+        self.spans = {}
+
+
+def solve(params, Q, p, A0, zl, zu, num_ineq, num_eq, T, sigma, scaling=True, scaling_iters=10,
+          keep_unscaled=True, history=False, packed=None, timer=None):
+    """Solve one batch; returns a dict with unscaled x/y/z, scaled state, final residuals.
+
+    Q[B,n,n], p[B,n,1], A0[B,m,n], zl/zu[B,m,1] fp32 device tensors (unscaled, Q already *2 as
+    main.py:718 loads it).  ``keep_unscaled=False`` scales the data in place (saves 8 GB at the
+    bench config) and reports residuals through the scaling identity instead of the originals.
+    """
+    params = param_dict(params)
+    B, n = Q.shape[0], Q.shape[1]
+    m = A0.shape[1]
+    if num_ineq + num_eq != m:
+        raise ValueError(f"num_ineq + num_eq = {num_ineq + num_eq} but A0 has {m} rows")
+    h = params["U_i"].shape[0]
+    if T > params["rho"].shape[0]:
+        raise ValueError(f"T={T} exceeds the model length {params['rho'].shape[0]} (models/lstm.py:60)")
+    dev = Q.device
+    N = n + m
+    timer = timer or Timer(False)
+    packed = packed or PackedWeights()
+    Upk, Wx = packed.get(params, h)
+    rho_p, alpha_p, b_h = (params[k].detach().contiguous() for k in ("rho", "alpha", "b_h"))
+
+    f32 = dict(dtype=torch.float32, device=dev)
+    tok = timer.start("scaling")
+    if scaling:
+        dst = None if keep_unscaled else (Q, p, A0, zl, zu)
+        Qs, ps, As, zls, zus, D, E, c = ops.ruiz_scale(Q, p, A0, zl, zu, scaling_iters, out=dst)
+    else:
+        Qs, ps, As, zls, zus = Q, p, A0, zl, zu
+        D = E = c = None
+    timer.stop(tok)
+
+    # state (two sets) and work buffers
+    xs = [torch.zeros(B, n, **f32), torch.empty(B, n, **f32)]
+    ys = [torch.zeros(B, m, **f32), torch.empty(B, m, **f32)]
+    zs = [torch.zeros(B, m, **f32), torch.empty(B, m, **f32)]
+    xvs = [torch.zeros(B, N, **f32), torch.empty(B, N, **f32)]
+    Hs = [torch.zeros(B, N, h, **f32), torch.empty(B, N, h, **f32)]
+    C = torch.zeros(B, N, h, **f32)
+    g = torch.empty(B, N, **f32)
+    part = torch.empty(ops.lstm_ntiles(h), B * N, **f32)
+    scal = torch.empty(ops.NSCAL, **f32)
+    pv, zlv, zuv = ps.reshape(B, n), zls.reshape(B, m), zus.reshape(B, m)
+    if history:
+        hist = torch.zeros(4, T, B, **f32)  # obj, ls_res, primal, dual
+        tmp = (torch.empty(B, n, **f32), torch.empty(B, m, **f32), torch.empty(B, m, **f32))
+
+    cur = 0
+    tok = timer.start("iterations")
+    for t in range(T):
+        nxt = 1 - cur
+        ops.schedule(rho_p, alpha_p, t, out=scal)
+        k = timer.start("k:kkt_resgrad")
+        ops.kkt_resgrad(Qs, As, pv, xs[cur], ys[cur], zs[cur], xvs[cur], sigma, scal, num_ineq, g=g)
+        timer.stop(k)
+        k = timer.start("k:lstm_cell")
+        ops.lstm_cell(Hs[cur], C, xvs[cur], g, Upk, Wx, Hn=Hs[nxt], Cn=C, part=part)
+        timer.stop(k)
+        ops.admm_update(n, m, num_ineq, part, b_h, xvs[cur], xs[cur], ys[cur], zs[cur], zlv, zuv, scal,
+                        out=(xvs[nxt], xs[nxt], ys[nxt], zs[nxt]))
+        if history:  # main.py:949-957 on unscaled data; kept on device
+            ops.kkt_lsres(Qs, As, pv, xs[cur], ys[cur], zs[cur], xvs[nxt], sigma, scal, num_ineq,
+                          out=hist[1, t])
+            if scaling:
+                ux, uy, uz = ops.unscale(D, E, c, xs[nxt], ys[nxt], zs[nxt], out=tmp)
+            else:
+                ux, uy, uz = xs[nxt], ys[nxt], zs[nxt]
+            o, pr, du = _metrics(Q, p, A0, Qs, ps, As, D, E, c, ux, uy, uz, xs[nxt], ys[nxt], zs[nxt],
+                                 keep_unscaled or not scaling)
+            hist[0, t].copy_(o)
+            hist[2, t].copy_(pr)
+            hist[3, t].copy_(du)
+        cur = nxt
+    timer.stop(tok)
+
+    tok = timer.start("unscale")
+    if scaling:
+        x, y, z = ops.unscale(D, E, c, xs[cur], ys[cur], zs[cur])
+    else:
+        x, y, z = xs[cur], ys[cur], zs[cur]
+    timer.stop(tok)
+
+    obj, pr, du = _metrics(Q, p, A0, Qs, ps, As, D, E, c, x, y, z, xs[cur], ys[cur], zs[cur],
+                           keep_unscaled or not scaling)
+    out = dict(x=x.unsqueeze(-1), y=y.unsqueeze(-1), z=z.unsqueeze(-1), xv=xvs[cur].unsqueeze(-1),
+               H=Hs[cur], C=C, x_scaled=xs[cur].unsqueeze(-1), y_scaled=ys[cur].unsqueeze(-1),
+               z_scaled=zs[cur].unsqueeze(-1), obj=obj, primal=pr, dual=du, scal=scal,
+               scaled=(Qs, ps, As, zls, zus), D=D, E=E, c=c)
+    if history:
+        out.update(hist_obj=hist[0], hist_ls_res=hist[1], hist_primal=hist[2], hist_dual=hist[3])
+    return out
+
+
+def _metrics(Q, p, A0, Qs, ps, As, D, E, c, x, y, z, xh, yh, zh, have_unscaled):
+    """Residuals on the unscaled problem (utils.py:53-54, 68-71).  Without the unscaled originals
+    the scaled data give the same quantities through the scaling identities
+      A0 x - z = E^-1 (Â x̂ - ẑ),  Qx + p + A0^T y = c^-1 D^-1 (Q̂ x̂ + p̂ + Â^T ŷ),  obj = c^-1 obĵ
+    (equal in exact arithmetic; rounding differs)."""
+    B, n = Qs.shape[0], Qs.shape[1]
+    if have_unscaled:
+        return ops.metrics(Q, p.reshape(B, n), A0, x, y, z)
+    m = As.shape[1]
+    obj_s, _, _ = ops.metrics(Qs, ps.reshape(B, n), As, xh, yh, zh)
+    prim = (ops.bmv(As, xh) - zh) / E
+    Aty = ops.kkt_matvec(Qs, As, torch.cat([torch.zeros_like(xh), yh], 1), 0.0, _unit_scal(Qs), m,
+                         transpose=True)[:, :n]
+    dual = ((ops.bmv(Qs, xh) + ps.reshape(B, n)) + Aty) / (c.reshape(B, 1) * D)
+    return obj_s / c, prim.norm(dim=1), dual.norm(dim=1)
+
+
+def _unit_scal(like):
+    s = torch.ones(ops.NSCAL, dtype=torch.float32, device=like.device)
+    return s

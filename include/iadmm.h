@@ -1,0 +1,160 @@
+/*
+ * iadmm.h — C-ABI of the MI355X-native I-ADMM-LSTM solve loop (libiadmm.so, gfx950).
+ *
+ * The reference (NetSysOpt/I-ADMM-LSTM) is pure PyTorch with no FFI; its operator API is the
+ * Python module surface ``models/lstm.py:LSTM.forward``, ``models/lu.py:LU.forward``,
+ * ``methods/scaling.py:Scaling.scale_data`` and ``utils.py:primal_dual_loss``.  Each entry point
+ * below replaces the ATen-op sequence named in its comment; the Python drop-ins under
+ * ``models/``, ``methods/`` and ``utils.py`` bind them through ``ctypes``.
+ *
+ * Conventions
+ *   - Every pointer is a DEVICE pointer to contiguous row-major fp32, batch-major
+ *     ([B][rows][cols]), unless documented as host.  Integers are int64_t sizes.
+ *   - ``stream`` is a hipStream_t passed as void* (0 = legacy default stream).  Calls are
+ *     stream-ordered and asynchronous: no allocation, no host synchronisation, no global mutable
+ *     state; safe to capture in a hipGraph and to call from several threads on distinct streams.
+ *   - Every buffer (outputs and workspaces) is caller-owned.
+ *   - Return value: 0 on success; a negative IADMM_E* code for a bad argument or a size beyond
+ *     a kernel's limit (nothing is launched); a positive hipError_t if a launch failed.
+ *     No C++ exception crosses this boundary.
+ *   - Iteration scalars (rho, 1/rho, alpha, ...) live in a small DEVICE buffer ``scal`` written by
+ *     iadmm_schedule, so a whole iteration runs without a host round trip.
+ */
+#ifndef IADMM_H
+#define IADMM_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum {
+  IADMM_OK = 0,
+  IADMM_E_ARG = -1,      /* null pointer / non-positive size                   */
+  IADMM_E_SIZE = -2,     /* size beyond the kernel's on-chip limit            */
+  IADMM_E_ALIGN = -3     /* pointer not 16-B aligned where the kernel needs it */
+};
+
+/* Layout of the per-iteration scalar buffer ``scal`` (IADMM_NSCAL floats, device). */
+enum {
+  IADMM_S_RHO_IN = 0,    /* sigmoid(rho[t])                        models/lstm.py:60   */
+  IADMM_S_RHO_EQ = 1,    /* rho * 1e3 on equality rows             models/lstm.py:18,62 */
+  IADMM_S_IRHO_IN = 2,   /* 1 / rho_in                             models/lstm.py:68-69 */
+  IADMM_S_IRHO_EQ = 3,   /* 1 / rho_eq                                                  */
+  IADMM_S_ALPHA = 4,     /* 2 * sigmoid(alpha[t])                  models/lstm.py:63   */
+  IADMM_S_1MALPHA = 5,   /* 1 - alpha                              models/lstm.py:88   */
+  IADMM_NSCAL = 8
+};
+
+/* Library / device info.  Returns the number of exported compute entry points. */
+int iadmm_version(void);
+
+/* Iteration scalars of step t from the raw parameters rho[T,1], alpha[T,1]
+ * (replaces models/lstm.py:60-63).  ``scal`` gets IADMM_NSCAL floats. */
+int iadmm_schedule(const float* rho_param, const float* alpha_param, int64_t t, float* scal,
+                   void* stream);
+
+/* Fixed-alpha scalars for Stage II (models/lu.py:24): copies rho entries of ``scal_in`` and
+ * sets alpha / 1-alpha from the host value. */
+int iadmm_schedule_fixed_alpha(const float* scal_in, float alpha, float* scal_out, void* stream);
+
+/* Implicit-KKT residual gradient  g = K^T (K xv - b~)  (replaces models/lstm.py:67-72: the
+ * K materialisation, the RHS and the two dependent bmm).  K is never formed:
+ *   K = [[Q + sigma I, A0^T], [A0, -diag(1/rho_vec)]],  b~ = [sigma x - p ; z - y / rho_vec].
+ * Q[B,n,n], A0[B,m,n], p/x[B,n], y/z[B,m], xv[B,n+m] -> g[B,n+m];
+ * btild[B,n+m] and rho_vec[B,m] are optional outputs (may be NULL).
+ * Rows [0,num_ineq) of A0 use rho_in, rows [num_ineq,m) rho_eq.
+ * Limit: 3n + 2m <= 40960 (on-chip vectors). */
+int iadmm_kkt_resgrad(int64_t B, int64_t n, int64_t m, int64_t num_ineq,
+                      const float* Q, const float* A0, const float* p,
+                      const float* x, const float* y, const float* z, const float* xv,
+                      float sigma, const float* scal,
+                      float* g, float* btild, float* rho_vec, void* stream);
+
+/* ||K xv - b~||_2 per instance (main.py:952 ``ls_res``), same implicit K. out[B]. */
+int iadmm_kkt_lsres(int64_t B, int64_t n, int64_t m, int64_t num_ineq,
+                    const float* Q, const float* A0, const float* p,
+                    const float* x, const float* y, const float* z, const float* xv,
+                    float sigma, const float* scal, float* out, void* stream);
+
+/* Implicit K v (transpose=0) or K^T v (transpose=1), v/out [B,n+m]; the operator behind the
+ * A_tild object the drop-in forward returns (models/lstm.py:96, used as bmm(A_tild, xv) at
+ * main.py:952).  Limit: 3n + 2m <= 40960. */
+int iadmm_kkt_matvec(int64_t B, int64_t n, int64_t m, int64_t num_ineq, const float* Q,
+                     const float* A0, const float* v, float sigma, const float* scal,
+                     int transpose, float* out, void* stream);
+
+/* Dense K[B,n+m,n+m] (models/lstm.py:67-68, models/lu.py:123-124): for Stage II and tests. */
+int iadmm_kkt_assemble(int64_t B, int64_t n, int64_t m, int64_t num_ineq, const float* Q,
+                       const float* A0, float sigma, const float* scal, float* K, void* stream);
+
+/* Pack the LSTM gate weights for the cell kernel (models/lstm.py:21-38 parameter layout).
+ * W_g[2,h], U_g[h,h], b_g[h] for g in (i,f,o,u), W_h[h,1].
+ * Upk: iadmm_lstm_packed_floats(h) floats; Wx: iadmm_lstm_wx_floats(h) floats. */
+int64_t iadmm_lstm_packed_floats(int64_t h);
+int64_t iadmm_lstm_wx_floats(int64_t h);
+int iadmm_lstm_pack(int64_t h,
+                    const float* W_i, const float* U_i, const float* b_i,
+                    const float* W_f, const float* U_f, const float* b_f,
+                    const float* W_o, const float* U_o, const float* b_o,
+                    const float* W_u, const float* U_u, const float* b_u,
+                    const float* W_h, float* Upk, float* Wx, void* stream);
+
+/* Number of hidden tiles (partial-projection slabs) the cell kernel writes. */
+int64_t iadmm_lstm_ntiles(int64_t h);
+
+/* Fused coordinate-wise LSTM cell over M = B*(n+m) rows (replaces models/lstm.py:74-80):
+ *   pre_g = [xv,g] W_g + H U_g + b_g ; I,F,O = sigmoid ; U = tanh
+ *   C' = I*U + F*C ; H' = O*tanh(C') ; part[tile][row] = sum_{j in tile} H'[row,j] W_h[j]
+ * H[M,h], C[M,h], xv[M], g[M] -> Hn[M,h], Cn[M,h], part[ntiles][M].
+ * Cn may alias C (in-place cell state); Hn must not alias H.
+ * The hidden x gate contraction runs on fp32 MFMA (v_mfma_f32_32x32x2_f32). */
+int iadmm_lstm_cell_fwd(int64_t M, int64_t h, const float* H, const float* C,
+                        const float* xv, const float* g, const float* Upk, const float* Wx,
+                        float* Hn, float* Cn, float* part, void* stream);
+
+/* ADMM update (replaces models/lstm.py:80 ``+ b_h`` and :82-94):
+ * grad = sum_tiles part + b_h ; xv' = xv - grad ; x' = alpha xv'[:n] + (1-alpha) x ;
+ * z~ = z + (v - y)/rho ; z' = clamp(z~ + y/rho, zl, zu) ; y' = y + rho (z~ - z').
+ * relax_z != 0 applies alpha to z as well (models/lu.py:138, Stage II); then ``part`` is NULL
+ * and ``xv`` already holds the solved xv'. Outputs must not alias inputs. rho_vec optional. */
+int iadmm_admm_update(int64_t B, int64_t n, int64_t m, int64_t num_ineq, int64_t ntiles,
+                      const float* part, const float* b_h, const float* xv,
+                      const float* x, const float* y, const float* z,
+                      const float* zl, const float* zu, const float* scal, int relax_z,
+                      float* xv_out, float* x_out, float* y_out, float* z_out,
+                      float* rho_vec, void* stream);
+
+/* Modified Ruiz equilibration + cost scaling, ``iters`` rounds (replaces
+ * methods/scaling.py:50-119 without its dense-diagonal bmm).  Inputs may alias outputs.
+ * Outputs: scaled Q,p,A0,zl,zu; diagonal vectors D[B,n], E[B,m]; c[B].
+ * Limit: 3n + 2m <= 40952. */
+int iadmm_ruiz_scale(int64_t B, int64_t n, int64_t m, int64_t iters,
+                     const float* Q, const float* p, const float* A0,
+                     const float* zl, const float* zu,
+                     float* Q_out, float* p_out, float* A0_out, float* zl_out, float* zu_out,
+                     float* D, float* E, float* c, void* stream);
+
+/* Unscale iterates (main.py:1025-1027): x=D x, y=(c^-1 E) y, z=E^-1 z.  May run in place. */
+int iadmm_unscale(int64_t B, int64_t n, int64_t m, const float* D, const float* E,
+                  const float* c, const float* x, const float* y, const float* z,
+                  float* x_out, float* y_out, float* z_out, void* stream);
+
+/* Metrics on one batch (utils.py:53-54, 68-71): obj = 1/2 x^T Q x + p^T x,
+ * primal = ||A0 x - z||_2, dual = ||Q x + p + A0^T y||_2; each out[B] (any may be NULL).
+ * Limit: 3n + 2m <= 40960. */
+int iadmm_metrics(int64_t B, int64_t n, int64_t m, const float* Q, const float* p,
+                  const float* A0, const float* x, const float* y, const float* z,
+                  float* obj, float* primal, float* dual, void* stream);
+
+/* Batched matvec with a metric epilogue (utils.py:56-63): out[B,R] =
+ *   mode 0: M x ; mode 1: max(M x - rhs, 0) (ineq_dist) ; mode 2: |rhs - M x| (eq_dist).
+ * M[B,R,C], x[B,C], rhs[B,R] (unused for mode 0).  Limit: R + C <= 40960. */
+int iadmm_bmv(int64_t B, int64_t R, int64_t C, const float* M, const float* x, const float* rhs,
+              int mode, float* out, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* IADMM_H */

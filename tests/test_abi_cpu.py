@@ -1,0 +1,52 @@
+"""CPU-side checks of the C-ABI boundary: the HIP library loads without a GPU and exports every
+entry point include/iadmm.h declares, with the argument counts the ctypes layer binds."""
+import os
+import re
+
+import pytest
+
+import iadmm_path  # noqa: F401
+from iadmm import _abi
+
+from conftest import REPO
+
+HEADER = os.path.join(REPO, "include", "iadmm.h")
+
+
+def declared():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return {m.group(1): m.group(2) for m in re.finditer(r"\b(iadmm_\w+)\s*\(([^)]*)\)\s*;", src)}
+
+
+def test_library_loads_and_exports_header_symbols():
+    lib = _abi.lib()
+    decl = declared()
+    assert len(decl) >= 15
+    missing = [name for name in decl if getattr(lib, name, None) is None]
+    assert not missing, f"declared in iadmm.h but not exported: {missing}"
+
+
+def test_ctypes_signatures_match_header_arity():
+    for name, args in declared().items():
+        assert name in _abi.SIGNATURES, f"{name} not bound in _abi.SIGNATURES"
+        n_header = 0 if args.strip() in ("", "void") else len(args.split(","))
+        assert len(_abi.SIGNATURES[name][1]) == n_header, name
+
+
+def test_size_queries_without_gpu():
+    lib = _abi.lib()
+    assert lib.iadmm_lstm_ntiles(800) == 25
+    assert lib.iadmm_lstm_ntiles(40) == 2
+    assert lib.iadmm_lstm_packed_floats(800) == 25 * 25 * 128 * 32
+    assert lib.iadmm_version() > 0
+
+
+def test_bad_arguments_rejected_before_launch():
+    # argument checks run on the host before any HIP call: safe without a GPU
+    with pytest.raises(_abi.IadmmError, match="bad argument"):
+        _abi.call("iadmm_kkt_resgrad", 0, 10, 10, 5, *([None] * 7), 1.0, None, None, None, None, None)
+    with pytest.raises(_abi.IadmmError, match="size beyond"):
+        _abi.call("iadmm_kkt_resgrad", 1, 20000, 20000, 0, *([1] * 7), 1.0, 1, 1, None, None, None)
+    with pytest.raises(_abi.IadmmError, match="bad argument"):
+        _abi.call("iadmm_lstm_cell_fwd", 10, 8, 16, 16, 16, 16, 16, 16, 16, 16, 16, None)

@@ -1,0 +1,86 @@
+"""Bench-shape parity and size-independent properties on the GPU.
+
+* n=1000, m=500+500, h=800 (BASELINE config 2 instance shape) on a few instances: HIP path vs
+  the CPU oracle for the Ruiz scaling and T=3 full iterations (rel-L2 1e-4 on x, H, C, residuals).
+* determinism: two solves of the same batch are bitwise identical (no atomics anywhere).
+* shard independence: instances solved in two shards are bitwise identical to one batch (the
+  multi-GPU path shards instances with no collective).
+"""
+import numpy as np
+import pytest
+import torch
+
+import iadmm_path  # noqa: F401
+from oracle import iadmm_oracle as orc
+
+pytestmark = pytest.mark.gpu
+
+
+def rel_l2(a, b):
+    a = torch.as_tensor(a).double().cpu()
+    b = torch.as_tensor(b).double().cpu()
+    return float((a - b).norm() / max(b.norm(), 1e-30))
+
+
+@pytest.fixture(scope="module")
+def bench_batch():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from iadmm import data
+    d = data.make_qp_batch(1000, 500, 500, 3, first_index=0, device="cuda")
+    params = data.init_lstm_params(800, 100, device="cuda")
+    return d, params
+
+
+def test_bench_shape_vs_oracle(bench_batch):
+    from iadmm import solver
+    d, params = bench_batch
+    T = 3
+    with torch.no_grad():
+        out = solver.solve(params, d["Q"], d["p"], d["A0"], d["zl"], d["zu"], 500, 500, T, 6e-6)
+    torch.set_num_threads(max(1, min(16, torch.get_num_threads())))
+    cpu = {k: v.cpu() for k, v in d.items()}
+    pc = {k: v.cpu() for k, v in params.items()}
+    with torch.no_grad():
+        ref = orc.solve(pc, cpu["Q"], cpu["p"], cpu["A0"], cpu["zl"], cpu["zu"], 500, 500, T, 6e-6, 800)
+    sc = ref["scaling"]
+    assert rel_l2(out["scaled"][0], sc["Q"]) < 1e-6
+    assert rel_l2(out["scaled"][2], sc["A0"]) < 1e-6
+    assert rel_l2(out["D"], torch.diagonal(sc["D"], dim1=1, dim2=2)) < 1e-6
+    for k in ("x", "y", "z", "xv"):
+        assert rel_l2(out[k], ref[k]) < 1e-4, k
+    assert rel_l2(out["H"], ref["H"]) < 1e-4
+    assert rel_l2(out["C"], ref["C"]) < 1e-4
+    np.testing.assert_allclose(out["primal"].cpu().numpy(), ref["primal"].numpy(), rtol=1e-4)
+    np.testing.assert_allclose(out["dual"].cpu().numpy(), ref["dual"].numpy(), rtol=1e-4)
+
+
+def test_bitwise_deterministic(bench_batch):
+    from iadmm import solver
+    d, params = bench_batch
+    with torch.no_grad():
+        a = solver.solve(params, d["Q"], d["p"], d["A0"], d["zl"], d["zu"], 500, 500, 4, 6e-6)
+        b = solver.solve(params, d["Q"], d["p"], d["A0"], d["zl"], d["zu"], 500, 500, 4, 6e-6)
+    for k in ("x", "y", "z", "H", "C", "primal", "dual"):
+        assert torch.equal(a[k], b[k]), k
+
+
+def test_shards_equal_full_batch(bench_batch):
+    from iadmm import solver
+    d, params = bench_batch
+    with torch.no_grad():
+        full = solver.solve(params, d["Q"], d["p"], d["A0"], d["zl"], d["zu"], 500, 500, 4, 6e-6)
+        parts = [solver.solve(params, *(d[k][s].contiguous() for k in ("Q", "p", "A0", "zl", "zu")),
+                              500, 500, 4, 6e-6) for s in (slice(0, 1), slice(1, 3))]
+    for k in ("x", "z", "primal", "dual"):
+        assert torch.equal(full[k], torch.cat([p[k] for p in parts])), k
+
+
+def test_generator_reproduces_shards():
+    from iadmm import data
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    a = data.make_qp_batch(64, 20, 12, 4, first_index=10, device="cuda")
+    b = data.make_qp_batch(64, 20, 12, 2, first_index=12, device="cuda")
+    for k in a:
+        assert torch.equal(a[k][2:], b[k]), k
