@@ -1,7 +1,8 @@
 """Bench-shape parity and size-independent properties on the GPU.
 
 * n=1000, m=500+500, h=800 (BASELINE config 2 instance shape) on a few instances: HIP path vs
-  the CPU oracle for the Ruiz scaling and T=3 full iterations (rel-L2 1e-4 on x, H, C, residuals).
+  the CPU oracle for the Ruiz scaling and T=3 full iterations (rel-L2 1e-4 on x, z, xv, H, C and
+  the residuals; 5e-3 on y, see the comment at the assertion).
 * determinism: two solves of the same batch are bitwise identical (no atomics anywhere).
 * shard independence: instances solved in two shards are bitwise identical to one batch (the
   multi-GPU path shards instances with no collective).
@@ -47,8 +48,12 @@ def test_bench_shape_vs_oracle(bench_batch):
     assert rel_l2(out["scaled"][0], sc["Q"]) < 1e-6
     assert rel_l2(out["scaled"][2], sc["A0"]) < 1e-6
     assert rel_l2(out["D"], torch.diagonal(sc["D"], dim1=1, dim2=2)) < 1e-6
-    for k in ("x", "y", "z", "xv"):
+    for k in ("x", "z", "xv"):
         assert rel_l2(out[k], ref[k]) < 1e-4, k
+    # y on equality rows is rho_eq (z~ - b) with rho_eq ~ 500 and z~ ~ b: the subtraction cancels
+    # ~3 of fp32's 7 digits, so y carries summation-order noise amplified ~1e3 (the reference has
+    # the same sensitivity to its BLAS order).  Bound: rel-L2 5e-3.
+    assert rel_l2(out["y"], ref["y"]) < 5e-3
     assert rel_l2(out["H"], ref["H"]) < 1e-4
     assert rel_l2(out["C"], ref["C"]) < 1e-4
     np.testing.assert_allclose(out["primal"].cpu().numpy(), ref["primal"].numpy(), rtol=1e-4)
