@@ -1,0 +1,44 @@
+"""Multi-GPU plumbing: one process per GPU, instance-batch sharding, no data-path collective.
+
+QP instances are independent and the LSTM weights are read-only at inference,
+so rank r solves the contiguous instance range ``shard(B_global, world, r)``; instance seeds are
+global indices, so a shard reproduces exactly the instances a single GPU would solve.  The only
+collectives are measurement (barrier, max-over-ranks time) and, for training, the gradient
+all-reduce.
+"""
+from __future__ import annotations
+
+import os
+
+import torch
+
+
+def env():
+    """(world, rank, local_rank) from the torch.distributed.run environment."""
+    return (int(os.environ.get("WORLD_SIZE", "1")), int(os.environ.get("RANK", "0")),
+            int(os.environ.get("LOCAL_RANK", "0")))
+
+
+def shard(global_batch, world, rank):
+    """Contiguous [start, start+count) of ``global_batch`` instances for ``rank`` (sizes differ by
+    at most one when the batch does not divide)."""
+    base, extra = divmod(int(global_batch), int(world))
+    start = rank * base + min(rank, extra)
+    return start, base + (1 if rank < extra else 0)
+
+
+def init(backend, local_rank=0):
+    import torch.distributed as dist
+    if backend == "nccl":
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    else:
+        dist.init_process_group(backend)
+    return dist
+
+
+def max_over_ranks(value, dist=None, device="cpu"):
+    if dist is None or not dist.is_initialized() or dist.get_world_size() == 1:
+        return float(value)
+    t = torch.tensor([float(value)], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t)

@@ -82,12 +82,14 @@ class Timer:
 
 
 def solve(params, Q, p, A0, zl, zu, num_ineq, num_eq, T, sigma, scaling=True, scaling_iters=10,
-          keep_unscaled=True, history=False, packed=None, timer=None):
+          keep_unscaled=True, history=False, packed=None, timer=None, iter_hook=None):
     """Solve one batch; returns a dict with unscaled x/y/z, scaled state, final residuals.
 
     Q[B,n,n], p[B,n,1], A0[B,m,n], zl/zu[B,m,1] fp32 device tensors (unscaled, Q already *2 as
     main.py:718 loads it).  ``keep_unscaled=False`` scales the data in place (saves 8 GB at the
     bench config) and reports residuals through the scaling identity instead of the originals.
+    ``history=True`` records per-iteration obj / ls_res / primal / dual on the device and calls
+    ``iter_hook(t, x, y, z)`` with the unscaled iterate ([B,n], [B,m], [B,m]) after each step.
     """
     params = param_dict(params)
     B, n = Q.shape[0], Q.shape[1]
@@ -154,6 +156,8 @@ def solve(params, Q, p, A0, zl, zu, num_ineq, num_eq, T, sigma, scaling=True, sc
             hist[0, t].copy_(o)
             hist[2, t].copy_(pr)
             hist[3, t].copy_(du)
+            if iter_hook is not None:  # extra per-iteration device metrics (main.py:959-978)
+                iter_hook(t, ux, uy, uz)
         cur = nxt
     timer.stop(tok)
 

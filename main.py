@@ -1,0 +1,187 @@
+"""Reference-compatible CLI (main.py / configs/QP.yaml of NetSysOpt/I-ADMM-LSTM), HIP-backed.
+
+Same flag names and YAML config as the reference (main.py:22-62; ``-c/--config`` YAML whose
+unknown keys are ignored like ``parse_known_args``), plus ``--weight_decay`` which the reference
+reads but never registers (main.py:191).  Implemented modes:
+
+  --test   the test loop of main.py:549-1268 for prob_type QP: load instances
+           (./datasets/QP_{n}_{ineq}_{eq}/qp_{id}.gz, the reference's gz-pickled dicts, or
+           ``--synthetic`` instances from the generate_data.py:67-76 distribution), Ruiz-scale,
+           ``test_outer_T`` Stage-I iterations, unscale, per-iteration report on unscaled data,
+           "Parallel Time" and the optional ``--save_sol`` .mat file.  All compute runs in
+           libiadmm.so kernels (iadmm/solver.py); per-iteration metrics stay on the device and
+           are copied once per batch.
+  (train)  not built yet: training needs the backward kernels.
+"""
+import argparse
+import gzip
+import os
+import pickle
+import random
+import sys
+import time
+
+import numpy as np
+import torch
+import yaml
+
+import iadmm_path  # noqa: F401
+from iadmm import data as qpdata
+from iadmm import ops, solver
+
+
+def build_parser():
+    p = argparse.ArgumentParser(description="train")
+    p.add_argument("-c", "--config", type=str)
+    add = p.add_argument
+    add("--num_var", type=int); add("--num_eq", type=int); add("--num_ineq", type=int)
+    add("--prob_type", type=str); add("--qplib_num", type=int)
+    add("--scaling_ites", type=int, default=10); add("--input_dim", type=int, default=2)
+    add("--hidden_dim", type=int); add("--model_name", type=str); add("--num_layer", type=int)
+    add("--sigma", type=float)
+    add("--eq_tol", type=float); add("--ineq_tol", type=float); add("--truncated_length", type=int)
+    add("--val_frac", type=float); add("--test_frac", type=float); add("--batch_size", type=int)
+    add("--device", type=str); add("--lr", type=float); add("--num_epoch", type=int)
+    add("--outer_T", type=int); add("--early_stop_mode", type=str)
+    add("--patience", type=int, default=100); add("--save_dir", type=str, default="./results/")
+    add("--save_sol", action="store_true"); add("--seed", type=int, default=17)
+    add("--scaling", action="store_true"); add("--test", action="store_true")
+    add("--test_outer_T", type=int); add("--test_batch_size", type=int); add("--data_size", type=int)
+    add("--feas_rest", action="store_true"); add("--feas_rest_num", type=int)
+    add("--weight_decay", type=float, default=0.0)
+    # build-only conveniences
+    add("--synthetic", action="store_true", help="generate instances instead of reading ./datasets")
+    add("--random_init", action="store_true", help="random-init weights when no checkpoint exists")
+    add("--data_dir", type=str, default="./datasets")
+    return p
+
+
+def parse_args(argv=None):
+    """configargparse semantics: YAML supplies defaults, command-line flags win, unknown keys
+    (YAML or CLI) are ignored (main.py:22-23, 65)."""
+    p = build_parser()
+    pre, _ = p.parse_known_args(argv)
+    if pre.config:
+        with open(pre.config) as f:
+            cfg = yaml.safe_load(f) or {}
+        known = {a.dest for a in p._actions}
+        p.set_defaults(**{k: v for k, v in cfg.items() if k in known})
+    args, _ = p.parse_known_args(argv)
+    return args
+
+
+def split_ids(args):
+    """main.py:171-183."""
+    random.seed(args.seed)
+    train_size = int(args.data_size * (1 - args.val_frac - args.test_frac))
+    val_size = int(args.data_size * args.val_frac)
+    ids = list(range(args.data_size))
+    random.shuffle(ids)
+    return ids[:train_size], ids[train_size:train_size + val_size], ids[train_size + val_size:]
+
+
+def load_qp_instances(args, ids, device):
+    """Reference on-disk format (main.py:621-722): one gzip-pickled dict per instance, Q doubled."""
+    path = os.path.join(args.data_dir, f"QP_{args.num_var}_{args.num_ineq}_{args.num_eq}")
+    keys = ("Q", "p", "A0", "zl", "zu", "G", "c", "A", "b")
+    cols = {k: [] for k in keys}
+    for i in ids:
+        with gzip.open(os.path.join(path, f"qp_{i}.gz"), "rb") as f:
+            d = pickle.load(f)  # user dataset in the reference's own format
+        for k in keys:
+            cols[k].append(d[k])
+    t = {k: torch.tensor(np.array(v), dtype=torch.float32, device=device) for k, v in cols.items()}
+    t["Q"] = t["Q"] * 2
+    return t
+
+
+def checkpoint_path(args, model_name="lstm"):
+    # main.py:557-561 (test side reads QP_{n}_{eq}_{ineq}_{T}_{h})
+    return os.path.join(args.save_dir, model_name, "params",
+                        f"QP_{args.num_var}_{args.num_eq}_{args.num_ineq}_{args.outer_T}_{args.hidden_dim}.pth")
+
+
+def run_test(args):
+    from models.lstm import LSTM
+    if args.prob_type != "QP":
+        raise SystemExit(f"prob_type {args.prob_type!r} is out of scope (DESIGN.md §0); use QP")
+    device = args.device or "cuda:0"
+    torch.cuda.set_device(torch.device(device))
+    mi, me, n = args.num_ineq, args.num_eq, args.num_var
+    model = LSTM(mi + me, args.input_dim, args.hidden_dim, args.outer_T, device)
+    ck = checkpoint_path(args, model.name())
+    if os.path.exists(ck):
+        model.load_state_dict(torch.load(ck, map_location=device, weights_only=True))
+    elif not args.random_init:
+        raise SystemExit(f"no checkpoint at {ck} (pass --random_init to run with random weights)")
+    model.eval()
+    _, _, test_ids = split_ids(args)
+    tb = args.test_batch_size
+    nb = len(test_ids) // tb
+    T = args.test_outer_T
+    packed = solver.PackedWeights()
+    reports, total_time, last = [], 0.0, None
+    with torch.no_grad():
+        if args.synthetic:
+            allq = qpdata.make_qp_batch(n, mi, me, nb * tb, first_index=0, seed=args.seed, device=device)
+            allq.update(G=allq["A0"][:, :mi], A=allq["A0"][:, mi:], c=allq["zu"][:, :mi], b=allq["zu"][:, mi:])
+        else:
+            allq = load_qp_instances(args, test_ids[:nb * tb], device)
+        for bi in range(nb):
+            sl = slice(bi * tb, (bi + 1) * tb)
+            d = {k: v[sl].contiguous() for k, v in allq.items()}
+            G, c, A, b = d["G"], d["c"].reshape(tb, -1), d["A"], d["b"].reshape(tb, -1)
+            viol = torch.zeros(4, T, tb, device=device)
+
+            def hook(t, x, y, z):  # main.py:959-968, kept on the device
+                if mi:
+                    iv = ops.bmv(G, x, c, ops.BMV_POS_EXCESS)
+                    viol[0, t], viol[1, t] = iv.max(1).values, iv.mean(1)
+                if me:
+                    ev = ops.bmv(A, x, b, ops.BMV_ABS_GAP)
+                    viol[2, t], viol[3, t] = ev.max(1).values, ev.mean(1)
+
+            timer = solver.Timer(True)
+            out = solver.solve(model, d["Q"], d["p"], d["A0"], d["zl"], d["zu"], mi, me, T, args.sigma,
+                               scaling=args.scaling, scaling_iters=args.scaling_ites, history=True,
+                               packed=packed, timer=timer, iter_hook=hook)
+            spans = timer.totals_ms()
+            total_time += sum(v for k, v in spans.items() if not k.startswith("k:")) / 1e3
+            h = {k: out["hist_" + k].mean(1).cpu().numpy() for k in ("obj", "ls_res", "primal", "dual")}
+            h["viol"] = viol.mean(2).cpu().numpy()
+            reports.append(h)
+            last = out
+    mean = lambda k: np.mean([r[k] for r in reports], axis=0)  # noqa: E731
+    obj, pr, du, vi = mean("obj"), mean("primal"), mean("dual"), mean("viol")
+    for t in range(T):  # main.py:1117-1138
+        print("Epoch : {} | Test_Obj : {:.3f}".format(t, obj[t]))
+        print("Primal_Residuals : {} | Dual_Residuals : {}".format(pr[t], du[t]))
+        if mi:
+            print("Test_Max_Ineq : {:.3f} | Test_Mean_Ineq : {:.3f} |".format(vi[0, t], vi[1, t]))
+        if me:
+            print("Test_Max_Eq : {:.3f} | Test_Mean_Eq : {:.3f} |".format(vi[2, t], vi[3, t]))
+    if args.feas_rest:
+        raise SystemExit("--feas_rest needs the Stage II LU kernels (not built yet, DESIGN.md §7)")
+    print("Parallel Time : {}".format(total_time / (nb * tb)))
+    if args.save_sol:  # main.py:1172-1178, 1248-1268
+        import scipy.io as sio
+        path = os.path.join(args.save_dir, "lstm", "QP_{}_{}_{}_{}_{}_results.mat".format(
+            args.num_var, args.num_eq, args.num_ineq, args.outer_T, args.hidden_dim))
+        os.makedirs(os.path.dirname(path), exist_ok=True)
+        sio.savemat(path, {"time": total_time, "x": last["x"].cpu().numpy(),
+                           "objs": np.array([r["obj"] for r in reports]),
+                           "ls_res": np.array([r["ls_res"] for r in reports]),
+                           "primal_res": np.array([r["primal"] for r in reports]),
+                           "dual_res": np.array([r["dual"] for r in reports])})
+    return reports, total_time
+
+
+def main(argv=None):
+    args = parse_args(argv)
+    if args.test:
+        return run_test(args)
+    raise SystemExit("training mode needs the backward kernels, which are not built yet (DESIGN.md §7)")
+
+
+if __name__ == "__main__":
+    main(sys.argv[1:])
