@@ -34,7 +34,7 @@ __global__ void schedule_fixed_kernel(const float* in, float alpha, float* out) 
 struct UpdArgs {
   int64_t B;
   int n, m, num_ineq, ntiles, relax_z;
-  const float *part, *bh, *xv, *x, *y, *z, *zl, *zu, *scal;
+  const float *part, *bh, *xv, *x, *y, *z, *zl, *zu, *scal, *rho_rows;
   float *xvo, *xo, *yo, *zo, *rhovec;
 };
 
@@ -65,7 +65,8 @@ __global__ __launch_bounds__(256) void admm_update_kernel(UpdArgs a) {
       const int j = i - a.n;
       const int64_t k = b * a.m + j;
       const bool ineq = j < a.num_ineq;
-      const float rho = ineq ? rho_in : rho_eq, irho = ineq ? irho_in : irho_eq;
+      float rho = ineq ? rho_in : rho_eq, irho = ineq ? irho_in : irho_eq;
+      if (a.rho_rows) { rho = a.rho_rows[k]; irho = 1.0f / rho; }  // explicit rho_vec (models/lu.py)
       const float y = a.y[k], z = a.z[k];
       const float zt = z + irho * (xvn - y);
       const float zr = a.relax_z ? alpha * zt + oma * z : zt;
@@ -104,7 +105,8 @@ extern "C" int iadmm_schedule_fixed_alpha(const float* scal_in, float alpha, flo
 extern "C" int iadmm_admm_update(int64_t B, int64_t n, int64_t m, int64_t num_ineq,
                                  int64_t ntiles, const float* part, const float* b_h,
                                  const float* xv, const float* x, const float* y, const float* z,
-                                 const float* zl, const float* zu, const float* scal, int relax_z,
+                                 const float* zl, const float* zu, const float* scal,
+                                 const float* rho_rows, int relax_z,
                                  float* xv_out, float* x_out, float* y_out, float* z_out,
                                  float* rho_vec, void* stream) {
   if (B <= 0 || n <= 0 || m < 0 || num_ineq < 0 || num_ineq > m) return IADMM_E_ARG;
@@ -113,7 +115,7 @@ extern "C" int iadmm_admm_update(int64_t B, int64_t n, int64_t m, int64_t num_in
   if (part && (!b_h || ntiles <= 0)) return IADMM_E_ARG;
   if (xv_out == xv || x_out == x || (m > 0 && (y_out == y || z_out == z))) return IADMM_E_ARG;
   UpdArgs a{B, (int)n, (int)m, (int)num_ineq, (int)ntiles, relax_z, part, b_h, xv, x, y, z, zl,
-            zu, scal, xv_out, x_out, y_out, z_out, rho_vec};
+            zu, scal, rho_rows, xv_out, x_out, y_out, z_out, rho_vec};
   const int64_t M = B * (n + m);
   const int64_t blocks = (M + 255) / 256;
   hipLaunchKernelGGL(admm_update_kernel, dim3((unsigned)(blocks < 8192 ? blocks : 8192)), dim3(256),

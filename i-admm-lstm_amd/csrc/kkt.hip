@@ -187,7 +187,7 @@ __global__ __launch_bounds__(kKktThreads) void bmv_kernel(int R, int C, const fl
 // Implicit K v (TRANS=false) or K^T v (TRANS=true): only the Q block differs.
 //   top = (Q or Q^T) v1 + sigma v1 + A0^T v2 ;  bottom = A0 v1 - v2 / rho
 template <int NG, bool VEC, bool TRANS>
-__global__ __launch_bounds__(kKktThreads) void kkt_matvec_kernel(KktArgs a, float* out) {
+__global__ __launch_bounds__(kKktThreads) void kkt_matvec_kernel(KktArgs a, const float* rho_rows, float* out) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   const int n = a.n, m = a.m, N = n + m;
   float* xs = sm;
@@ -208,23 +208,25 @@ __global__ __launch_bounds__(kKktThreads) void kkt_matvec_kernel(KktArgs a, floa
   else sweep<NG, VEC, true, false>(a.Q + b * n * n, n, n, xs, nullptr, t1, col, wave, nw, lane);
   if (m > 0) sweep<NG, VEC, true, true>(a.A0 + b * m * n, m, n, xs, vs, t3, col, wave, nw, lane);
   col_reduce<NG, VEC>(col, red, n, wave, nw, lane);
-  const float irho_in = a.scal[IADMM_S_IRHO_IN], irho_eq = a.scal[IADMM_S_IRHO_EQ];
+  const float irho_in = a.scal ? a.scal[IADMM_S_IRHO_IN] : 0.f;
+  const float irho_eq = a.scal ? a.scal[IADMM_S_IRHO_EQ] : 0.f;
   for (int i = tid; i < n; i += blockDim.x) {
     // TRANS: red already holds Q^T v1 + A0^T v2 (one column accumulator)
     out[b * N + i] = TRANS ? red[i] + a.sigma * xs[i] : (t1[i] + a.sigma * xs[i]) + red[i];
   }
   for (int j = tid; j < m; j += blockDim.x) {
-    const float irho = j < a.num_ineq ? irho_in : irho_eq;
+    const float irho = rho_rows ? 1.0f / rho_rows[b * m + j] : (j < a.num_ineq ? irho_in : irho_eq);
     out[b * N + n + j] = t3[j] + (-irho) * vs[j];
   }
 }
 
 // Dense K (models/lstm.py:67-68, models/lu.py:123-124) for Stage II and explicit inspection.
 __global__ void kkt_assemble_kernel(int64_t B, int n, int m, int num_ineq, const float* Q,
-                                    const float* A0, float sigma, const float* scal, float* K) {
+                                    const float* A0, float sigma, const float* scal,
+                                    const float* rho_rows, float* K) {
   const int N = n + m;
   const int64_t tot = B * (int64_t)N * N;
-  const float irho_in = scal[IADMM_S_IRHO_IN], irho_eq = scal[IADMM_S_IRHO_EQ];
+  const float irho_in = scal ? scal[IADMM_S_IRHO_IN] : 0.f, irho_eq = scal ? scal[IADMM_S_IRHO_EQ] : 0.f;
   for (int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; k < tot;
        k += (int64_t)gridDim.x * blockDim.x) {
     const int64_t b = k / ((int64_t)N * N);
@@ -234,7 +236,9 @@ __global__ void kkt_assemble_kernel(int64_t B, int n, int m, int num_ineq, const
     if (i < n && j < n) v = Q[(b * n + i) * n + j] + (i == j ? sigma : 0.f);
     else if (i < n) v = A0[(b * m + (j - n)) * n + i];
     else if (j < n) v = A0[(b * m + (i - n)) * n + j];
-    else v = (i == j) ? -((i - n) < num_ineq ? irho_in : irho_eq) : -0.f;
+    else if (i != j) v = -0.f;
+    else if (rho_rows) v = -(1.0f / rho_rows[b * m + (i - n)]);
+    else v = -((i - n) < num_ineq ? irho_in : irho_eq);
     K[k] = v;
   }
 }
@@ -328,9 +332,9 @@ extern "C" int iadmm_bmv(int64_t B, int64_t R, int64_t C, const float* Mx, const
 
 extern "C" int iadmm_kkt_matvec(int64_t B, int64_t n, int64_t m, int64_t num_ineq, const float* Q,
                                 const float* A0, const float* v, float sigma, const float* scal,
-                                int transpose, float* out, void* stream) {
+                                const float* rho_rows, int transpose, float* out, void* stream) {
   if (B <= 0 || n <= 0 || m < 0 || num_ineq < 0 || num_ineq > m) return IADMM_E_ARG;
-  if (!Q || !v || !scal || !out || (m > 0 && !A0)) return IADMM_E_ARG;
+  if (!Q || !v || !out || (m > 0 && !A0) || (m > 0 && !scal && !rho_rows)) return IADMM_E_ARG;
   if (!kkt_fits(n, m) || B > 0x7fffffff) return IADMM_E_SIZE;
   KktArgs a{(int)n, (int)m, (int)num_ineq, Q, A0, nullptr, nullptr, nullptr, nullptr, v, sigma, scal,
             nullptr, nullptr, nullptr, nullptr};
@@ -339,23 +343,24 @@ extern "C" int iadmm_kkt_matvec(int64_t B, int64_t n, int64_t m, int64_t num_ine
   const size_t lds = (3 * n + 2 * m) * sizeof(float);
   hipStream_t s = (hipStream_t)stream;
   if (transpose) {
-    IADMM_DISPATCH_NG(ng, vec, { hipLaunchKernelGGL((kkt_matvec_kernel<NG_, V_, true>), dim3((unsigned)B), dim3(kKktThreads), lds, s, a, out); });
+    IADMM_DISPATCH_NG(ng, vec, { hipLaunchKernelGGL((kkt_matvec_kernel<NG_, V_, true>), dim3((unsigned)B), dim3(kKktThreads), lds, s, a, rho_rows, out); });
   } else {
-    IADMM_DISPATCH_NG(ng, vec, { hipLaunchKernelGGL((kkt_matvec_kernel<NG_, V_, false>), dim3((unsigned)B), dim3(kKktThreads), lds, s, a, out); });
+    IADMM_DISPATCH_NG(ng, vec, { hipLaunchKernelGGL((kkt_matvec_kernel<NG_, V_, false>), dim3((unsigned)B), dim3(kKktThreads), lds, s, a, rho_rows, out); });
   }
   IADMM_CHECK_LAUNCH();
   return 0;
 }
 
 extern "C" int iadmm_kkt_assemble(int64_t B, int64_t n, int64_t m, int64_t num_ineq, const float* Q,
-                                  const float* A0, float sigma, const float* scal, float* K,
-                                  void* stream) {
-  if (B <= 0 || n <= 0 || m < 0 || num_ineq < 0 || num_ineq > m || !Q || !scal || !K || (m > 0 && !A0))
+                                  const float* A0, float sigma, const float* scal,
+                                  const float* rho_rows, float* K, void* stream) {
+  if (B <= 0 || n <= 0 || m < 0 || num_ineq < 0 || num_ineq > m || !Q || !K || (m > 0 && !A0))
     return IADMM_E_ARG;
+  if (m > 0 && !scal && !rho_rows) return IADMM_E_ARG;
   const int64_t tot = B * (n + m) * (n + m);
   const int64_t blocks = (tot + 255) / 256;
   hipLaunchKernelGGL(kkt_assemble_kernel, dim3((unsigned)(blocks < 16384 ? blocks : 16384)), dim3(256), 0,
-                     (hipStream_t)stream, B, (int)n, (int)m, (int)num_ineq, Q, A0, sigma, scal, K);
+                     (hipStream_t)stream, B, (int)n, (int)m, (int)num_ineq, Q, A0, sigma, scal, rho_rows, K);
   IADMM_CHECK_LAUNCH();
   return 0;
 }

@@ -25,16 +25,17 @@ SIGNATURES = {
     "iadmm_lstm_ntiles": (i64, [i64]),
     "iadmm_lstm_pack": (cint, [i64] + [vp] * 13 + [vp, vp, vp]),
     "iadmm_lstm_cell_fwd": (cint, [i64, i64, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp]),
-    "iadmm_admm_update": (cint, [i64, i64, i64, i64, i64, vp, vp, vp, vp, vp, vp, vp, vp, vp, cint,
+    "iadmm_admm_update": (cint, [i64, i64, i64, i64, i64, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, cint,
                                  vp, vp, vp, vp, vp, vp]),
     "iadmm_ruiz_scale": (cint, [i64, i64, i64, i64, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp]),
     "iadmm_unscale": (cint, [i64, i64, i64, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp]),
     "iadmm_metrics": (cint, [i64, i64, i64, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp]),
     "iadmm_bmv": (cint, [i64, i64, i64, vp, vp, vp, cint, vp, vp]),
     "iadmm_lu_factor": (cint, [i64, i64, vp, vp, vp, vp]),
-    "iadmm_lu_solve": (cint, [i64, i64, vp, vp, vp, vp, vp]),
-    "iadmm_kkt_assemble": (cint, [i64, i64, i64, i64, vp, vp, f32, vp, vp, vp]),
-    "iadmm_kkt_matvec": (cint, [i64, i64, i64, i64, vp, vp, vp, f32, vp, cint, vp, vp]),
+    "iadmm_lu_solve": (cint, [i64, i64, vp, vp, vp, vp]),
+    "iadmm_kkt_assemble": (cint, [i64, i64, i64, i64, vp, vp, f32, vp, vp, vp, vp]),
+    "iadmm_kkt_rhs": (cint, [i64, i64, i64, i64, vp, vp, vp, vp, f32, vp, vp, vp, vp]),
+    "iadmm_kkt_matvec": (cint, [i64, i64, i64, i64, vp, vp, vp, f32, vp, vp, cint, vp, vp]),
 }
 
 ERRORS = {-1: "bad argument", -2: "size beyond kernel limit", -3: "misaligned pointer"}

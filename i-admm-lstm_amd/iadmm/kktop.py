@@ -13,10 +13,11 @@ from . import ops
 
 
 class KKTOperator:
-    def __init__(self, Q, A0, sigma, scal, num_ineq, transposed=False):
+    def __init__(self, Q, A0, sigma, scal, num_ineq, transposed=False, rho_rows=None):
         self.Q, self.A0, self.sigma, self.scal = Q, A0, float(sigma), scal
         self.num_ineq = int(num_ineq)
         self.transposed = transposed
+        self.rho_rows = rho_rows  # explicit per-row rho (Stage II); else two-class rho from scal
         B, n = Q.shape[0], Q.shape[1]
         N = n + A0.shape[1]
         self.shape = torch.Size((B, N, N))
@@ -28,7 +29,8 @@ class KKTOperator:
         dims = tuple(dims[0]) if len(dims) == 1 and isinstance(dims[0], (tuple, list)) else dims
         if tuple(dims) != (0, 2, 1):
             raise NotImplementedError("KKTOperator only supports permute(0, 2, 1)")
-        return KKTOperator(self.Q, self.A0, self.sigma, self.scal, self.num_ineq, not self.transposed)
+        return KKTOperator(self.Q, self.A0, self.sigma, self.scal, self.num_ineq, not self.transposed,
+                           self.rho_rows)
 
     def transpose(self, d0, d1):
         if {d0 % 3, d1 % 3} != {1, 2}:
@@ -49,13 +51,13 @@ class KKTOperator:
         if v.dim() != 3 or v.shape[-1] != 1:
             raise NotImplementedError("KKTOperator.bmm supports [B,N,1] right-hand sides")
         out = ops.kkt_matvec(self.Q, self.A0, v.reshape(v.shape[0], -1).contiguous(), self.sigma,
-                             self.scal, self.num_ineq, transpose=self.transposed)
+                             self.scal, self.num_ineq, transpose=self.transposed, rho_rows=self.rho_rows)
         return out.unsqueeze(-1)
 
     __matmul__ = bmm
 
     def dense(self):
-        K = ops.kkt_assemble(self.Q, self.A0, self.sigma, self.scal, self.num_ineq)
+        K = ops.kkt_assemble(self.Q, self.A0, self.sigma, self.scal, self.num_ineq, rho_rows=self.rho_rows)
         return K.transpose(1, 2).contiguous() if self.transposed else K
 
     def to_dense(self):

@@ -105,7 +105,7 @@ def lstm_cell(H, C, xv, g, Upk, Wx, Hn=None, Cn=None, part=None):
 
 # --------------------------------------------------------------------------- ADMM update
 def admm_update(n, m, num_ineq, part, b_h, xv, x, y, z, zl, zu, scal, relax_z=False, out=None,
-                rho_vec=None):
+                rho_vec=None, rho_rows=None):
     """xv' / x' / z' / y' (models/lstm.py:80-94; relax_z -> models/lu.py:133-140)."""
     B = x.shape[0]
     if out is None:
@@ -113,7 +113,7 @@ def admm_update(n, m, num_ineq, part, b_h, xv, x, y, z, zl, zu, scal, relax_z=Fa
     xvo, xo, yo, zo = out
     ntiles = 0 if part is None else part.shape[0]
     _abi.call("iadmm_admm_update", B, n, m, int(num_ineq), ntiles, _p(part), _p(b_h), _p(xv), _p(x), _p(y),
-              _p(z), _p(zl), _p(zu), _p(scal), int(bool(relax_z)), _p(xvo), _p(xo), _p(yo), _p(zo),
+              _p(z), _p(zl), _p(zu), _p(scal), _p(rho_rows), int(bool(relax_z)), _p(xvo), _p(xo), _p(yo), _p(zo),
               _p(rho_vec), _stream())
     return xvo, xo, yo, zo
 
@@ -167,21 +167,50 @@ def bmv(Mx, x, rhs=None, mode=BMV_PLAIN):
     return out
 
 
-def kkt_matvec(Q, A0, v, sigma, scal, num_ineq, transpose=False):
+def kkt_matvec(Q, A0, v, sigma, scal, num_ineq, transpose=False, rho_rows=None):
     """Implicit K v or K^T v, v[B,n+m] -> [B,n+m]."""
     B, n = Q.shape[0], Q.shape[1]
     m = A0.shape[1]
     out = empty(B, n + m, like=Q)
     _abi.call("iadmm_kkt_matvec", B, n, m, int(num_ineq), _p(Q), _p(A0), _p(v), float(sigma), _p(scal),
-              int(bool(transpose)), _p(out), _stream())
+              _p(rho_rows), int(bool(transpose)), _p(out), _stream())
     return out
 
 
-def kkt_assemble(Q, A0, sigma, scal, num_ineq):
-    """Dense K[B,n+m,n+m]."""
+def kkt_assemble(Q, A0, sigma, scal, num_ineq, rho_rows=None):
+    """Dense K[B,n+m,n+m] (rho per class from ``scal`` or per row from ``rho_rows`` [B,m])."""
     B, n = Q.shape[0], Q.shape[1]
     m = A0.shape[1]
     K = empty(B, n + m, n + m, like=Q)
-    _abi.call("iadmm_kkt_assemble", B, n, m, int(num_ineq), _p(Q), _p(A0), float(sigma), _p(scal), _p(K),
-              _stream())
+    _abi.call("iadmm_kkt_assemble", B, n, m, int(num_ineq), _p(Q), _p(A0), float(sigma), _p(scal),
+              _p(rho_rows), _p(K), _stream())
     return K
+
+
+def kkt_rhs(p, x, y, z, sigma, scal=None, num_ineq=0, rho_rows=None, out=None):
+    """b~ = [sigma x - p ; z - y / rho], [B,n+m] (models/lu.py:125)."""
+    B, n = x.shape[0], x.shape[1]
+    m = y.shape[1]
+    out = empty(B, n + m, like=x) if out is None else out
+    _abi.call("iadmm_kkt_rhs", B, n, m, int(num_ineq), _p(p), _p(x), _p(y), _p(z), float(sigma), _p(scal),
+              _p(rho_rows), _p(out), _stream())
+    return out
+
+
+def lu_factor(K):
+    """In-place batched LU with partial pivoting: returns (LU (= K), piv int32 [B,N], info int32 [B])."""
+    B, N = K.shape[0], K.shape[1]
+    piv = torch.empty(B, N, dtype=torch.int32, device=K.device)
+    info = torch.empty(B, dtype=torch.int32, device=K.device)
+    _abi.call("iadmm_lu_factor", B, N, _p(K), piv.data_ptr(), info.data_ptr(), _stream())
+    return K, piv, info
+
+
+def lu_solve(LU, piv, b):
+    """Solve with (LU, piv) in place on a copy of b [B,N]; returns x."""
+    B, N = LU.shape[0], LU.shape[1]
+    x = b.clone().contiguous()
+    if piv.dtype != torch.int32 or not piv.is_contiguous():
+        raise TypeError("piv must be contiguous int32")
+    _abi.call("iadmm_lu_solve", B, N, _p(LU), piv.data_ptr(), _p(x), _stream())
+    return x

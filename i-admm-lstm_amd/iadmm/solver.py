@@ -199,3 +199,40 @@ def _metrics(Q, p, A0, Qs, ps, As, D, E, c, x, y, z, xh, yh, zh, have_unscaled):
 def _unit_scal(like):
     s = torch.ones(ops.NSCAL, dtype=torch.float32, device=like.device)
     return s
+
+
+STAGE2_ALPHA = 1.6  # models/lu.py:24
+
+
+def fixed_alpha_scal(alpha, device):
+    """Iteration scalars carrying only a fixed relaxation (Stage II): alpha, fl32(1 - alpha)."""
+    a = torch.tensor(alpha, dtype=torch.float32)
+    s = torch.zeros(ops.NSCAL, dtype=torch.float32)
+    s[ops.S_ALPHA] = a
+    s[ops.S_1MALPHA] = 1.0 - a
+    return s.to(device)
+
+
+def stage2(Q, p, A0, zl, zu, rho_rows, x, y, z, sigma, iters, alpha=STAGE2_ALPHA, timer=None):
+    """Stage II feasibility restoration (models/lu.py:13-47, driver main.py:1035-1066):
+    factor K once (rho of the last Stage-I iteration), then ``iters`` exact ADMM steps with
+    alpha-relaxation on x and z.  Works on the unscaled data like the reference.
+    Q[B,n,n], p[B,n], A0[B,m,n], zl/zu/rho_rows[B,m], x[B,n], y/z[B,m].  Returns the iterates and
+    the factors (LU, piv)."""
+    timer = timer or Timer(False)
+    B, n = x.shape
+    m = y.shape[1]
+    scal = fixed_alpha_scal(alpha, x.device)
+    tok = timer.start("stage2_factor")
+    K = ops.kkt_assemble(Q, A0, sigma, None, 0, rho_rows=rho_rows)
+    LU, piv, info = ops.lu_factor(K)
+    timer.stop(tok)
+    tok = timer.start("stage2_iterations")
+    xv = None
+    for _ in range(iters):
+        b = ops.kkt_rhs(p, x, y, z, sigma, rho_rows=rho_rows)
+        xs = ops.lu_solve(LU, piv, b)
+        xv, x, y, z = ops.admm_update(n, m, 0, None, None, xs, x, y, z, zl, zu, scal, relax_z=True,
+                                      rho_rows=rho_rows)
+    timer.stop(tok)
+    return dict(x=x, y=y, z=z, xv=xv, LU=LU, piv=piv, info=info)

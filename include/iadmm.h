@@ -80,14 +80,31 @@ int iadmm_kkt_lsres(int64_t B, int64_t n, int64_t m, int64_t num_ineq,
 
 /* Implicit K v (transpose=0) or K^T v (transpose=1), v/out [B,n+m]; the operator behind the
  * A_tild object the drop-in forward returns (models/lstm.py:96, used as bmm(A_tild, xv) at
- * main.py:952).  Limit: 3n + 2m <= 40960. */
+ * main.py:952).  rho per class from ``scal`` or per row from ``rho_rows`` [B,m] when non-NULL.
+ * Limit: 3n + 2m <= 40960. */
 int iadmm_kkt_matvec(int64_t B, int64_t n, int64_t m, int64_t num_ineq, const float* Q,
                      const float* A0, const float* v, float sigma, const float* scal,
-                     int transpose, float* out, void* stream);
+                     const float* rho_rows, int transpose, float* out, void* stream);
 
-/* Dense K[B,n+m,n+m] (models/lstm.py:67-68, models/lu.py:123-124): for Stage II and tests. */
+/* Dense K[B,n+m,n+m] (models/lstm.py:67-68, models/lu.py:123-124): for Stage II and tests.
+ * rho from ``scal`` (two classes) or per row from ``rho_rows`` [B,m] when non-NULL. */
 int iadmm_kkt_assemble(int64_t B, int64_t n, int64_t m, int64_t num_ineq, const float* Q,
-                       const float* A0, float sigma, const float* scal, float* K, void* stream);
+                       const float* A0, float sigma, const float* scal, const float* rho_rows,
+                       float* K, void* stream);
+
+/* b~ = [sigma x - p ; z - y / rho] (models/lu.py:125,129) into out[B,n+m]; rho as above. */
+int iadmm_kkt_rhs(int64_t B, int64_t n, int64_t m, int64_t num_ineq, const float* p,
+                  const float* x, const float* y, const float* z, float sigma,
+                  const float* scal, const float* rho_rows, float* out, void* stream);
+
+/* Stage II batched LU with partial pivoting, in place (replaces torch.lu, models/lu.py:31):
+ * A[B,N,N] -> packed L\U; piv[B,N] int32, 0-based (row i was swapped with piv[i]);
+ * info[B] = first 1-based zero pivot or 0.  Blocked right-looking, panel 16 (limit N <= 2400). */
+int iadmm_lu_factor(int64_t B, int64_t N, float* A, int* piv, int* info, void* stream);
+
+/* Solve with the factors in place (replaces torch.lu_solve, models/lu.py:32,35): x[B,N] holds b
+ * on entry and the solution on exit.  Limit N <= 12000. */
+int iadmm_lu_solve(int64_t B, int64_t N, const float* LU, const int* piv, float* x, void* stream);
 
 /* Pack the LSTM gate weights for the cell kernel (models/lstm.py:21-38 parameter layout).
  * W_g[2,h], U_g[h,h], b_g[h] for g in (i,f,o,u), W_h[h,1].
@@ -118,11 +135,14 @@ int iadmm_lstm_cell_fwd(int64_t M, int64_t h, const float* H, const float* C,
  * grad = sum_tiles part + b_h ; xv' = xv - grad ; x' = alpha xv'[:n] + (1-alpha) x ;
  * z~ = z + (v - y)/rho ; z' = clamp(z~ + y/rho, zl, zu) ; y' = y + rho (z~ - z').
  * relax_z != 0 applies alpha to z as well (models/lu.py:138, Stage II); then ``part`` is NULL
- * and ``xv`` already holds the solved xv'. Outputs must not alias inputs. rho_vec optional. */
+ * and ``xv`` already holds the solved xv'.  ``rho_rows`` [B,m] (optional) overrides the two-class
+ * rho of ``scal`` per row (the explicit rho_vec of models/lu.py:13).  Outputs must not alias
+ * inputs. rho_vec (optional output) receives the rho used per row. */
 int iadmm_admm_update(int64_t B, int64_t n, int64_t m, int64_t num_ineq, int64_t ntiles,
                       const float* part, const float* b_h, const float* xv,
                       const float* x, const float* y, const float* z,
-                      const float* zl, const float* zu, const float* scal, int relax_z,
+                      const float* zl, const float* zu, const float* scal,
+                      const float* rho_rows, int relax_z,
                       float* xv_out, float* x_out, float* y_out, float* z_out,
                       float* rho_vec, void* stream);
 
