@@ -1,0 +1,200 @@
+// Generic fp32-MFMA GEMMs for the training backward of the LSTM cell (models/lstm.py:74-80).
+//
+//   gemm_nt : out[M, Ni] (+)= X[M, K] . W[Ni, K]^T      (dH = dP . U_cat^T, K = 4h)
+//   gemm_tn : out[Ni, No]  = X[M, Ni]^T . Y[M, No]      (dU_cat = H^T . dP, split over M)
+//
+// gemm_nt uses the forward cell kernel's tiling (workgroup = 128 outputs x 256 rows, wave = 128
+// outputs x 64 rows = 8 accumulators of v_mfma_f32_32x32x2_f32, K staged 32-deep through padded
+// LDS, one 16-B LDS read per operand fragment).  gemm_tn contracts over the long row dimension:
+// a workgroup owns a 128 x 128 output tile and a contiguous slice of rows, stages [32 rows x 128]
+// of both operands in LDS (both are row-major along the output dims, so one fragment element per
+// lane is a conflict-free ds_read_b32) and writes an fp32 partial slab; iadmm_slab_reduce sums the
+// slabs in a fixed order (deterministic, no atomics).
+#include "common.h"
+
+namespace iadmm {
+
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+
+constexpr int kGBK = 32;
+constexpr int kGLD = kGBK + 4;
+
+template <bool ACC>
+__global__ __launch_bounds__(256, 2) void gemm_nt_kernel(int64_t M, int Ni, int K, const float* X,
+                                                         const float* W, float* out) {
+  __shared__ __attribute__((aligned(16))) float sA[128 * kGLD];
+  __shared__ __attribute__((aligned(16))) float sB[256 * kGLD];
+  const int nit = (Ni + 127) / 128;
+  const int it = blockIdx.x % nit;
+  const int64_t rt = blockIdx.x / nit;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, jl = lane & 31, hf = lane >> 5;
+  const int i0 = it * 128;
+  const int64_t r0 = rt * 256;
+  floatx16 acc[4][2];
+#pragma unroll
+  for (int g = 0; g < 4; ++g)
+#pragma unroll
+    for (int r = 0; r < 2; ++r)
+#pragma unroll
+      for (int q = 0; q < 16; ++q) acc[g][r][q] = 0.f;
+  const int nkc = (K + kGBK - 1) / kGBK;
+  for (int kc = 0; kc < nkc; ++kc) {
+    __syncthreads();
+    for (int idx = tid; idx < 128 * kGBK; idx += 256) {
+      const int row = idx / kGBK, kk = idx % kGBK, k = kc * kGBK + kk, i = i0 + row;
+      sA[row * kGLD + kk] = (i < Ni && k < K) ? W[(int64_t)i * K + k] : 0.f;
+    }
+    for (int idx = tid; idx < 256 * kGBK; idx += 256) {
+      const int row = idx / kGBK, kk = idx % kGBK, k = kc * kGBK + kk;
+      const int64_t r = r0 + row;
+      sB[row * kGLD + kk] = (r < M && k < K) ? X[r * K + k] : 0.f;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int G = 0; G < kGBK / 8; ++G) {
+      float4 af[4], bf[2];
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+        af[g] = *reinterpret_cast<const float4*>(&sA[(g * 32 + jl) * kGLD + 8 * G + 4 * hf]);
+#pragma unroll
+      for (int r = 0; r < 2; ++r)
+        bf[r] = *reinterpret_cast<const float4*>(&sB[(wave * 64 + r * 32 + jl) * kGLD + 8 * G + 4 * hf]);
+#pragma unroll
+      for (int s = 0; s < 4; ++s)
+#pragma unroll
+        for (int g = 0; g < 4; ++g)
+#pragma unroll
+          for (int r = 0; r < 2; ++r)
+            acc[g][r] = __builtin_amdgcn_mfma_f32_32x32x2f32(get4(af[g], s), get4(bf[r], s), acc[g][r], 0, 0, 0);
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < 2; ++r) {
+    const int64_t R = r0 + wave * 64 + r * 32 + jl;
+    if (R >= M) continue;
+#pragma unroll
+    for (int g = 0; g < 4; ++g)
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const int i = i0 + g * 32 + (q & 3) + 8 * (q >> 2) + 4 * hf;
+        if (i < Ni) {
+          float* o = out + R * Ni + i;
+          *o = ACC ? *o + acc[g][r][q] : acc[g][r][q];
+        }
+      }
+  }
+}
+
+// Partial slab of X[rows, Ni]^T . Y[rows, No] for the row slice of blockIdx.z.
+__global__ __launch_bounds__(256, 2) void gemm_tn_kernel(int64_t M, int Ni, int No, int64_t rows_per_split,
+                                                         const float* X, const float* Y, float* slab) {
+  __shared__ float sX[kGBK][128 + 4];
+  __shared__ float sY[kGBK][128 + 4];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, jl = lane & 31, hf = lane >> 5;
+  const int i0 = blockIdx.x * 128, o0 = blockIdx.y * 128;
+  const int64_t rbeg = (int64_t)blockIdx.z * rows_per_split;
+  const int64_t rend = min(M, rbeg + rows_per_split);
+  const int wi = (wave >> 1) * 64, wo = (wave & 1) * 64;  // wave tile 64 (i) x 64 (o)
+  floatx16 acc[2][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+      for (int q = 0; q < 16; ++q) acc[a][c][q] = 0.f;
+  for (int64_t rc = rbeg; rc < rend; rc += kGBK) {
+    __syncthreads();
+    for (int idx = tid; idx < kGBK * 128; idx += 256) {
+      const int rr = idx / 128, cc = idx % 128;
+      const int64_t r = rc + rr;
+      const bool ok = r < rend;
+      sX[rr][cc] = (ok && i0 + cc < Ni) ? X[r * Ni + i0 + cc] : 0.f;
+      sY[rr][cc] = (ok && o0 + cc < No) ? Y[r * No + o0 + cc] : 0.f;
+    }
+    __syncthreads();
+#pragma unroll 4
+    for (int ks = 0; ks < kGBK / 2; ++ks) {
+      const int kk = 2 * ks + hf;
+      float av[2], bv[2];
+#pragma unroll
+      for (int a = 0; a < 2; ++a) av[a] = sX[kk][wi + a * 32 + jl];
+#pragma unroll
+      for (int c = 0; c < 2; ++c) bv[c] = sY[kk][wo + c * 32 + jl];
+#pragma unroll
+      for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int c = 0; c < 2; ++c)
+          acc[a][c] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[a], bv[c], acc[a][c], 0, 0, 0);
+    }
+  }
+  float* S = slab + (int64_t)blockIdx.z * Ni * No;
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const int i = i0 + wi + a * 32 + (q & 3) + 8 * (q >> 2) + 4 * hf;
+        const int o = o0 + wo + c * 32 + jl;
+        if (i < Ni && o < No) S[(int64_t)i * No + o] = acc[a][c][q];
+      }
+}
+
+// out[e] (+)= sum_{s < nsplit} slab[s][e]  (fixed order)
+__global__ void slab_reduce_kernel(int64_t nelem, int nsplit, const float* slab, float* out, int acc) {
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < nelem; e += (int64_t)gridDim.x * blockDim.x) {
+    float s = 0.f;
+    for (int k = 0; k < nsplit; ++k) s += slab[(int64_t)k * nelem + e];
+    out[e] = acc ? out[e] + s : s;
+  }
+}
+
+}  // namespace iadmm
+
+using namespace iadmm;
+
+extern "C" int iadmm_gemm_nt(int64_t M, int64_t Ni, int64_t K, const float* X, const float* W,
+                             float* out, int accumulate, void* stream) {
+  if (M <= 0 || Ni <= 0 || K <= 0 || !X || !W || !out) return IADMM_E_ARG;
+  const int64_t nit = (Ni + 127) / 128, nrt = (M + 255) / 256;
+  if (nit * nrt > 0x7fffffffLL || Ni > (1 << 20) || K > (1 << 20)) return IADMM_E_SIZE;
+  const dim3 grid((unsigned)(nit * nrt));
+  if (accumulate)
+    hipLaunchKernelGGL(gemm_nt_kernel<true>, grid, dim3(256), 0, (hipStream_t)stream, M, (int)Ni, (int)K, X, W, out);
+  else
+    hipLaunchKernelGGL(gemm_nt_kernel<false>, grid, dim3(256), 0, (hipStream_t)stream, M, (int)Ni, (int)K, X, W, out);
+  IADMM_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int64_t iadmm_gemm_tn_splits(int64_t M, int64_t rows_per_split) {
+  return (M + rows_per_split - 1) / rows_per_split;
+}
+
+extern "C" int iadmm_gemm_tn(int64_t M, int64_t Ni, int64_t No, int64_t rows_per_split, const float* X,
+                             const float* Y, float* slab, float* out, int accumulate, void* stream) {
+  if (M <= 0 || Ni <= 0 || No <= 0 || rows_per_split <= 0 || !X || !Y || !slab || !out) return IADMM_E_ARG;
+  if (rows_per_split % kGBK) return IADMM_E_ARG;
+  const int64_t ns = (M + rows_per_split - 1) / rows_per_split;
+  if (ns > 65535 || Ni > (1 << 20) || No > (1 << 20)) return IADMM_E_SIZE;
+  hipStream_t s = (hipStream_t)stream;
+  const dim3 grid((unsigned)((Ni + 127) / 128), (unsigned)((No + 127) / 128), (unsigned)ns);
+  hipLaunchKernelGGL(gemm_tn_kernel, grid, dim3(256), 0, s, M, (int)Ni, (int)No, rows_per_split, X, Y, slab);
+  IADMM_CHECK_LAUNCH();
+  const int64_t nelem = Ni * No;
+  const int64_t blocks = (nelem + 255) / 256;
+  hipLaunchKernelGGL(slab_reduce_kernel, dim3((unsigned)(blocks < 4096 ? blocks : 4096)), dim3(256), 0, s,
+                     nelem, (int)ns, slab, out, accumulate);
+  IADMM_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int iadmm_slab_reduce(int64_t nelem, int64_t nsplit, const float* slab, float* out, int accumulate,
+                                 void* stream) {
+  if (nelem <= 0 || nsplit <= 0 || !slab || !out) return IADMM_E_ARG;
+  const int64_t blocks = (nelem + 255) / 256;
+  hipLaunchKernelGGL(slab_reduce_kernel, dim3((unsigned)(blocks < 4096 ? blocks : 4096)), dim3(256), 0,
+                     (hipStream_t)stream, nelem, (int)nsplit, slab, out, accumulate);
+  IADMM_CHECK_LAUNCH();
+  return 0;
+}

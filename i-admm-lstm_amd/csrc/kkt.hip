@@ -15,7 +15,7 @@ struct KktArgs {
   const float *Q, *A0, *p, *x, *y, *z, *xv;
   float sigma;
   const float* scal;
-  float *g, *btild, *rhovec, *lsres;
+  float *g, *btild, *rhovec, *lsres, *rout;
 };
 
 // One workgroup = one instance.  LDS: xs[n] (x~ -> r1), vs[m] (v -> r2), t1[n], t3[m], red[n].
@@ -57,6 +57,7 @@ __global__ __launch_bounds__(kKktThreads) void kkt_kernel(KktArgs a) {
     const float b1 = sigma * a.x[b * n + i] - a.p[b * n + i];
     const float r1 = ((t1[i] + sigma * xs[i]) + red[i]) - b1;
     if (a.btild) a.btild[b * N + i] = b1;
+    if (a.rout) a.rout[b * N + i] = r1;
     if (PASS2) xs[i] = r1; else ss += r1 * r1;
   }
   for (int j = tid; j < m; j += blockDim.x) {
@@ -65,6 +66,7 @@ __global__ __launch_bounds__(kKktThreads) void kkt_kernel(KktArgs a) {
     const float b2 = a.z[b * m + j] - irho * a.y[b * m + j];
     const float r2 = (t3[j] + (-irho) * vs[j]) - b2;
     if (a.btild) a.btild[b * N + n + j] = b2;
+    if (a.rout) a.rout[b * N + n + j] = r2;
     if (a.rhovec) a.rhovec[b * m + j] = rho;
     if (PASS2) vs[j] = r2; else ss += r2 * r2;
   }
@@ -265,11 +267,11 @@ extern "C" int iadmm_kkt_resgrad(int64_t B, int64_t n, int64_t m, int64_t num_in
                                  const float* Q, const float* A0, const float* p, const float* x,
                                  const float* y, const float* z, const float* xv, float sigma,
                                  const float* scal, float* g, float* btild, float* rho_vec,
-                                 void* stream) {
+                                 float* r_out, void* stream) {
   if (B <= 0 || n <= 0 || m < 0 || num_ineq < 0 || num_ineq > m) return IADMM_E_ARG;
   if (!Q || !p || !x || !xv || !scal || !g || (m > 0 && (!A0 || !y || !z))) return IADMM_E_ARG;
   if (!kkt_fits(n, m) || B > 0x7fffffff) return IADMM_E_SIZE;
-  KktArgs a{(int)n, (int)m, (int)num_ineq, Q, A0, p, x, y, z, xv, sigma, scal, g, btild, rho_vec, nullptr};
+  KktArgs a{(int)n, (int)m, (int)num_ineq, Q, A0, p, x, y, z, xv, sigma, scal, g, btild, rho_vec, nullptr, r_out};
   return launch_kkt<true>(B, n, m, a, (hipStream_t)stream);
 }
 
@@ -280,7 +282,7 @@ extern "C" int iadmm_kkt_lsres(int64_t B, int64_t n, int64_t m, int64_t num_ineq
   if (B <= 0 || n <= 0 || m < 0 || num_ineq < 0 || num_ineq > m) return IADMM_E_ARG;
   if (!Q || !p || !x || !xv || !scal || !out || (m > 0 && (!A0 || !y || !z))) return IADMM_E_ARG;
   if (!kkt_fits(n, m) || B > 0x7fffffff) return IADMM_E_SIZE;
-  KktArgs a{(int)n, (int)m, (int)num_ineq, Q, A0, p, x, y, z, xv, sigma, scal, nullptr, nullptr, nullptr, out};
+  KktArgs a{(int)n, (int)m, (int)num_ineq, Q, A0, p, x, y, z, xv, sigma, scal, nullptr, nullptr, nullptr, out, nullptr};
   return launch_kkt<false>(B, n, m, a, (hipStream_t)stream);
 }
 
@@ -337,7 +339,7 @@ extern "C" int iadmm_kkt_matvec(int64_t B, int64_t n, int64_t m, int64_t num_ine
   if (!Q || !v || !out || (m > 0 && !A0) || (m > 0 && !scal && !rho_rows)) return IADMM_E_ARG;
   if (!kkt_fits(n, m) || B > 0x7fffffff) return IADMM_E_SIZE;
   KktArgs a{(int)n, (int)m, (int)num_ineq, Q, A0, nullptr, nullptr, nullptr, nullptr, v, sigma, scal,
-            nullptr, nullptr, nullptr, nullptr};
+            nullptr, nullptr, nullptr, nullptr, nullptr};
   const int ng = ng_for(n);
   const bool vec = (n % 4 == 0) && aligned16(Q) && (m == 0 || aligned16(A0));
   const size_t lds = (3 * n + 2 * m) * sizeof(float);

@@ -17,17 +17,9 @@
 // prefetched into registers while the MFMAs run.  Workgroups are remapped XCD-aware so the njt
 // hidden tiles of one 256-row H panel run back to back on the same XCD (panel read from HBM once,
 // then served by that XCD's L2).
-#include "common.h"
+#include "cell_tile.h"
 
 namespace iadmm {
-
-typedef float floatx16 __attribute__((ext_vector_type(16)));
-
-constexpr int kJT = 32;          // hidden units per workgroup
-constexpr int kRows = 256;       // data rows per workgroup
-constexpr int kBK = 32;          // K chunk
-constexpr int kLD = kBK + 4;     // padded LDS row (floats)
-constexpr int kWxF = 16;         // packed per-unit fields: Wi0 Wi1 bi Wf0 Wf1 bf Wo0 Wo1 bo Wu0 Wu1 bu Wh
 
 inline int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
 
@@ -82,13 +74,8 @@ __global__ __launch_bounds__(256, 2) void lstm_cell_kernel(CellArgs a) {
   __shared__ __attribute__((aligned(16))) float sB[kRows * kLD];
   __shared__ __attribute__((aligned(16))) float sW[kWxF * kJT];
 
-  // XCD-aware bijective remap: blocks b, b+8, ... share an XCD; give each XCD a contiguous run
-  // of logical tiles with the hidden tile fastest, so an H panel is reused from that XCD's L2.
-  const int nwg = gridDim.x, bid = blockIdx.x;
-  const int xcd = bid & 7, local = bid >> 3, q8 = nwg >> 3, r8 = nwg & 7;
-  const int logical = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + local;
-  const int jt = logical % a.njt;
-  const int rt = logical / a.njt;
+  int jt, rt;
+  cell_tile_of_block(a.njt, jt, rt);
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int jl = lane & 31, hf = lane >> 5;
@@ -102,70 +89,8 @@ __global__ __launch_bounds__(256, 2) void lstm_cell_kernel(CellArgs a) {
   }
 
   floatx16 acc[4][2];
-#pragma unroll
-  for (int g = 0; g < 4; ++g)
-#pragma unroll
-    for (int r = 0; r < 2; ++r)
-#pragma unroll
-      for (int q = 0; q < 16; ++q) acc[g][r][q] = 0.f;
-
-  float4 ra[4], rb[8];
-  const float* Ubase = a.Upk + (int64_t)jt * a.nkc * 128 * kBK;
-  auto gload = [&](int kc) {
-    const float4* Ac = reinterpret_cast<const float4*>(Ubase + (int64_t)kc * 128 * kBK);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) ra[i] = Ac[tid + 256 * i];
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int idx = tid + 256 * i, row = idx >> 3, c4 = idx & 7;
-      const int64_t R = rbase + row;
-      const int k = kc * kBK + c4 * 4;
-      if constexpr (VEC) {
-        rb[i] = (R < M && k < h) ? *reinterpret_cast<const float4*>(a.H + R * h + k)
-                                 : make_float4(0.f, 0.f, 0.f, 0.f);
-      } else {
-        float4 t;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) set4(t, e, (R < M && k + e < h) ? a.H[R * h + k + e] : 0.f);
-        rb[i] = t;
-      }
-    }
-  };
-
-  gload(0);
-  for (int kc = 0; kc < a.nkc; ++kc) {
-    __syncthreads();
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int idx = tid + 256 * i, row = idx >> 3, c4 = idx & 7;
-      *reinterpret_cast<float4*>(&sA[row * kLD + c4 * 4]) = ra[i];
-    }
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int idx = tid + 256 * i, row = idx >> 3, c4 = idx & 7;
-      *reinterpret_cast<float4*>(&sB[row * kLD + c4 * 4]) = rb[i];
-    }
-    __syncthreads();
-    if (kc + 1 < a.nkc) gload(kc + 1);
-#pragma unroll
-    for (int G = 0; G < kBK / 8; ++G) {
-      float4 af[4], bf[2];
-#pragma unroll
-      for (int g = 0; g < 4; ++g)
-        af[g] = *reinterpret_cast<const float4*>(&sA[(g * 32 + jl) * kLD + 8 * G + 4 * hf]);
-#pragma unroll
-      for (int r = 0; r < 2; ++r)
-        bf[r] = *reinterpret_cast<const float4*>(&sB[(wave * 64 + r * 32 + jl) * kLD + 8 * G + 4 * hf]);
-#pragma unroll
-      for (int s = 0; s < 4; ++s)
-#pragma unroll
-        for (int g = 0; g < 4; ++g)
-#pragma unroll
-          for (int r = 0; r < 2; ++r)
-            acc[g][r] = __builtin_amdgcn_mfma_f32_32x32x2f32(get4(af[g], s), get4(bf[r], s),
-                                                             acc[g][r], 0, 0, 0);
-    }
-  }
+  cell_mainloop<VEC>(a.H, M, h, a.nkc, a.Upk + (int64_t)jt * a.nkc * 128 * kBK, rbase, sA, sB, acc, tid,
+                     wave, jl, hf);
 
   // ---- epilogue: gates, cell update, projection partial (all in registers)
   // accumulator element q of lane (jl,hf): hidden jj = (q&3) + 8*(q>>2) + 4*hf, data row jl.

@@ -1,0 +1,484 @@
+// Training backward of one I-ADMM-LSTM iteration and of the unsupervised loss
+// (reference: autograd through models/lstm.py:47-96 and utils.py:68-71, driven by
+// main.py:336-358).  Every reduction is a fixed-order slab / per-block partial: gradients are
+// bitwise reproducible.
+//
+// Forward of iteration t (per instance; rho_j = s*kappa_j, s = sigmoid(rho[t]), kappa = 1 on
+// inequality rows, 1e3 on equality rows, iota = 1/rho, a = 2 sigmoid(alpha[t])):
+//   r = K xv - b~,  g = K^T r,  in = [xv, g],  P_g = in W_g + H U_g + b_g,
+//   C' = I*U + F*C,  H' = O*tanh(C'),  q = H' W_h + b_h,  xv' = xv - q,
+//   x' = a x~' + (1-a) x,  zt = z + iota(v' - y),  z' = max(min(zt + iota y, zu), zl),
+//   y' = y + rho (zt - z').
+// Backward kernels (in the order the Python autograd Function calls them):
+//   admm_update_bwd   adjoints through x', z', y', xv' -> dq, partial dx/dy/dz, d(xv) pass-through,
+//                     and per-block partials of ds (through rho and iota), da and db_h
+//   lstm_cell_bwd     recomputes the gate pre-activations on MFMA (same tile as the forward) and
+//                     writes dP[M][4h], dC, per-row-tile W_h-gradient slabs and per-hidden-tile
+//                     partials of d(in) = dP W^T
+//   (gemm.hip)        dH = dP U_cat^T ; [dU_cat ; dW ; db] = [H, xv, g, 1]^T dP
+//   in_reduce         sums the d(in) partials: d(xv) += din0, dg = din1
+//   kkt_bwd           dr = K dg, d(xv) += K^T dr, dx -= sigma dr1, dz -= dr2, dy += iota dr2 and
+//                     diota = -dg2 r2 + dr2 (y - v)   (two sweeps of Q and A0, like the forward)
+//   sched_bwd         drho[t] = s(1-s) ds, dalpha[t] = 2 sig'(alpha_t) da, db_h
+//   loss_grad         ||A0x-z|| + ||Qx+p+A0^T y|| per instance and its gradient (two sweeps)
+#include "cell_tile.h"
+#include "sweep.h"
+
+namespace iadmm {
+
+// ------------------------------------------------------------------ ADMM update backward
+struct UpdBwdArgs {
+  int64_t B;
+  int n, m, num_ineq;
+  const float *x, *y, *z, *xvn, *zl, *zu, *scal;            // forward inputs / output xv'
+  const float *dx, *dy, *dz, *dxv;                          // adjoints of x', y', z', xv' (may be NULL)
+  float *dx_o, *dy_o, *dz_o, *dxv_o, *dq;                   // outputs
+  float* partials;                                          // [gridDim.x][4]: ds, da, dbh, 0
+};
+
+IADMM_DEV float dmin_a(float a, float b) { return a < b ? 1.f : (a == b ? 0.5f : 0.f); }  // d min(a,b)/da
+IADMM_DEV float dmax_a(float a, float b) { return a > b ? 1.f : (a == b ? 0.5f : 0.f); }  // d max(a,b)/da
+
+__global__ __launch_bounds__(256) void admm_update_bwd_kernel(UpdBwdArgs a) {
+  __shared__ float red[8];
+  const int N = a.n + a.m;
+  const int64_t M = a.B * (int64_t)N;
+  const float rho_in = a.scal[IADMM_S_RHO_IN], rho_eq = a.scal[IADMM_S_RHO_EQ];
+  const float irho_in = a.scal[IADMM_S_IRHO_IN], irho_eq = a.scal[IADMM_S_IRHO_EQ];
+  const float alpha = a.scal[IADMM_S_ALPHA], oma = a.scal[IADMM_S_1MALPHA];
+  float ds = 0.f, da = 0.f, dbh = 0.f;
+  for (int64_t R = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; R < M; R += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t b = R / N;
+    const int i = (int)(R - b * N);
+    float dxvt = a.dxv ? a.dxv[R] : 0.f;  // adjoint of xv' (total for this row)
+    if (i < a.n) {
+      const int64_t k = b * a.n + i;
+      const float dxp = a.dx ? a.dx[k] : 0.f;
+      dxvt += alpha * dxp;
+      a.dx_o[k] = oma * dxp;
+      da += dxp * (a.xvn[R] - a.x[k]);
+    } else {
+      const int j = i - a.n;
+      const int64_t k = b * a.m + j;
+      const bool ineq = j < a.num_ineq;
+      const float rho = ineq ? rho_in : rho_eq, iota = ineq ? irho_in : irho_eq;
+      const float kappa = ineq ? 1.f : 1e3f;
+      const float y = a.y[k], z = a.z[k], v = a.xvn[R];
+      const float zt = z + iota * (v - y);
+      const float w = zt + iota * y;
+      const float u1 = tmin(w, a.zu[k]);
+      const float zn = tmax(u1, a.zl[k]);
+      const float dyp = a.dy ? a.dy[k] : 0.f;
+      const float dzp = a.dz ? a.dz[k] : 0.f;
+      // y' = y + rho (zt - z')
+      float dyo = dyp, dzt = rho * dyp, drho = dyp * (zt - zn);
+      const float dzn = dzp - rho * dyp;
+      // z' = max(min(w, zu), zl)
+      const float dw = dzn * dmax_a(u1, a.zl[k]) * dmin_a(w, a.zu[k]);
+      // w = zt + iota y
+      dzt += dw;
+      dyo += iota * dw;
+      float diota = dw * y;
+      // zt = z + iota (v - y)
+      const float dzo = dzt;
+      const float dv = iota * dzt;
+      dyo -= iota * dzt;
+      diota += dzt * (v - y);
+      dxvt += dv;
+      drho += -diota / (rho * rho);
+      ds += kappa * drho;
+      a.dy_o[k] = dyo;
+      a.dz_o[k] = dzo;
+    }
+    a.dxv_o[R] = dxvt;   // xv' = xv - q: d(xv) gets the total adjoint ...
+    a.dq[R] = -dxvt;     // ... and q gets its negative
+    dbh += -dxvt;
+  }
+  const float s_ds = block_sum(ds, red);
+  const float s_da = block_sum(da, red);
+  const float s_dbh = block_sum(dbh, red);
+  if (threadIdx.x == 0) {
+    a.partials[blockIdx.x * 4 + 0] = s_ds;
+    a.partials[blockIdx.x * 4 + 1] = s_da;
+    a.partials[blockIdx.x * 4 + 2] = s_dbh;
+    a.partials[blockIdx.x * 4 + 3] = 0.f;
+  }
+}
+
+// ------------------------------------------------------------------ LSTM cell backward
+struct CellBwdArgs {
+  int64_t M;
+  int h, njt, nkc, nrt;
+  const float *H, *C, *xv, *g, *Upk, *Wx;
+  const float *dq, *dHn, *dCn;      // adjoint of q (per row), of H', of C' (NULL = 0)
+  float *dC, *dP;                   // adjoint of C (may alias dCn), dP[M][4h]
+  float *whslab;                    // [nrt][h]: sum over the tile's rows of H' * dq
+  float *inpart;                    // [njt][M][2]: sum over the tile's units of dP W^T
+};
+
+template <bool VEC>
+__global__ __launch_bounds__(256, 2) void lstm_cell_bwd_kernel(CellBwdArgs a) {
+  __shared__ __attribute__((aligned(16))) float sA[128 * kLD];
+  __shared__ __attribute__((aligned(16))) float sB[kRows * kLD];
+  __shared__ __attribute__((aligned(16))) float sW[kWxF * kJT];
+  __shared__ float swh[4][kJT];
+  int jt, rt;
+  cell_tile_of_block(a.njt, jt, rt);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, jl = lane & 31, hf = lane >> 5;
+  const int h = a.h;
+  const int64_t M = a.M;
+  const int64_t rbase = (int64_t)rt * kRows;
+  for (int i = tid; i < kWxF * kJT; i += 256) {
+    const int f = i / kJT, jj = i % kJT;
+    sW[i] = a.Wx[(int64_t)(jt * kJT + jj) * kWxF + f];
+  }
+  floatx16 acc[4][2];
+  cell_mainloop<VEC>(a.H, M, h, a.nkc, a.Upk + (int64_t)jt * a.nkc * 128 * kBK, rbase, sA, sB, acc, tid,
+                     wave, jl, hf);
+
+  float whp[16];
+#pragma unroll
+  for (int q = 0; q < 16; ++q) whp[q] = 0.f;
+#pragma unroll
+  for (int r = 0; r < 2; ++r) {
+    const int64_t R = rbase + wave * 64 + r * 32 + jl;
+    const bool rok = R < M;
+    const float in0 = rok ? a.xv[R] : 0.f;
+    const float in1 = rok ? a.g[R] : 0.f;
+    const float dq = rok ? a.dq[R] : 0.f;
+    float din0 = 0.f, din1 = 0.f;
+#pragma unroll
+    for (int qq = 0; qq < 4; ++qq) {
+      const int jj0 = 8 * qq + 4 * hf;
+      float4 wv[13];
+#pragma unroll
+      for (int f = 0; f < 13; ++f) wv[f] = *reinterpret_cast<const float4*>(&sW[f * kJT + jj0]);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int q = qq * 4 + e;
+        const int j = jt * kJT + jj0 + e;
+        const bool ok = rok && j < h;
+        const int64_t o = R * h + j;
+        float pre[4];
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const float xw = in0 * get4(wv[3 * g], e) + in1 * get4(wv[3 * g + 1], e);
+          pre[g] = (xw + acc[g][r][q]) + get4(wv[3 * g + 2], e);
+        }
+        const float ig = sigmoidf_(pre[0]), fg = sigmoidf_(pre[1]), og = sigmoidf_(pre[2]);
+        const float ug = tanhf(pre[3]);
+        const float cin = ok ? a.C[o] : 0.f;
+        const float c2 = ig * ug + fg * cin;
+        const float tc = tanhf(c2);
+        const float h2 = og * tc;
+        const float wh = get4(wv[12], e);
+        const float dHt = (ok && a.dHn ? a.dHn[o] : 0.f) + dq * wh;
+        const float dO = dHt * tc;
+        const float dCt = (ok && a.dCn ? a.dCn[o] : 0.f) + dHt * og * (1.f - tc * tc);
+        const float dI = dCt * ug, dU = dCt * ig, dF = dCt * cin;
+        const float dPi = dI * ig * (1.f - ig), dPf = dF * fg * (1.f - fg);
+        const float dPo = dO * og * (1.f - og), dPu = dU * (1.f - ug * ug);
+        if (ok) {
+          a.dC[o] = dCt * fg;
+          float* dp = a.dP + R * (int64_t)(4 * h) + j;
+          dp[0] = dPi; dp[h] = dPf; dp[2 * h] = dPo; dp[3 * h] = dPu;
+          whp[q] += h2 * dq;
+          din0 += dPi * get4(wv[0], e) + dPf * get4(wv[3], e) + dPo * get4(wv[6], e) + dPu * get4(wv[9], e);
+          din1 += dPi * get4(wv[1], e) + dPf * get4(wv[4], e) + dPo * get4(wv[7], e) + dPu * get4(wv[10], e);
+        }
+      }
+    }
+    din0 += __shfl_xor(din0, 32, 64);
+    din1 += __shfl_xor(din1, 32, 64);
+    if (hf == 0 && rok) {
+      a.inpart[((int64_t)jt * M + R) * 2 + 0] = din0;
+      a.inpart[((int64_t)jt * M + R) * 2 + 1] = din1;
+    }
+  }
+  // W_h gradient slab: sum of H' dq over this tile's 256 rows for its 32 units (fixed order)
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    float v = whp[q];
+#pragma unroll
+    for (int o = 1; o < 32; o <<= 1) v += __shfl_xor(v, o, 64);  // over the 32 rows of a half
+    whp[q] = v;
+  }
+  if (jl == 0) {
+#pragma unroll
+    for (int q = 0; q < 16; ++q) swh[wave][(q & 3) + 8 * (q >> 2) + 4 * hf] = whp[q];
+  }
+  __syncthreads();
+  if (tid < kJT) {
+    const int j = jt * kJT + tid;
+    if (j < h) a.whslab[(int64_t)rt * h + j] = ((swh[0][tid] + swh[1][tid]) + swh[2][tid]) + swh[3][tid];
+  }
+}
+
+// d(xv)[R] += sum_jt inpart[jt][R][0];  dg[R] = sum_jt inpart[jt][R][1]
+__global__ void in_reduce_kernel(int64_t M, int njt, const float* inpart, float* dxv, float* dg) {
+  for (int64_t R = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; R < M; R += (int64_t)gridDim.x * blockDim.x) {
+    float s0 = 0.f, s1 = 0.f;
+    for (int t = 0; t < njt; ++t) {
+      s0 += inpart[((int64_t)t * M + R) * 2 + 0];
+      s1 += inpart[((int64_t)t * M + R) * 2 + 1];
+    }
+    dxv[R] += s0;
+    dg[R] = s1;
+  }
+}
+
+// ------------------------------------------------------------------ KKT backward
+struct KktBwdArgs {
+  int n, m, num_ineq;
+  const float *Q, *A0, *xv, *y, *r, *dg;   // r = forward residual K xv - b~ (saved)
+  float sigma;
+  const float* scal;
+  float *dxv, *dx, *dy, *dz;                // accumulated in place
+  float* ds_inst;                           // [B] partial ds of this instance
+};
+
+// dr = K dg ; d(xv) += K^T dr ; dx -= sigma dr1 ; dz -= dr2 ; dy += iota dr2 ;
+// diota = -dg2 r2 + dr2 (y - v)  ->  ds += kappa * (-diota / rho^2)
+template <int NG, bool VEC>
+__global__ __launch_bounds__(256) void kkt_bwd_kernel(KktBwdArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  const int n = a.n, m = a.m, N = n + m;
+  float* us = sm;        // n : dg1 -> dr1
+  float* ws = us + n;    // m : dg2 -> dr2
+  float* t1 = ws + m;    // n
+  float* t3 = t1 + n;    // m
+  float* red = t3 + m;   // n
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, nw = blockDim.x >> 6;
+  const size_t b = blockIdx.x;
+  const float* Qb = a.Q + b * n * n;
+  const float* Ab = a.A0 + b * m * n;
+  for (int i = tid; i < N; i += blockDim.x) {
+    if (i < n) us[i] = a.dg[b * N + i]; else ws[i - n] = a.dg[b * N + i];
+  }
+  __syncthreads();
+  const float sigma = a.sigma;
+  const float rho_in = a.scal[IADMM_S_RHO_IN], rho_eq = a.scal[IADMM_S_RHO_EQ];
+  const float irho_in = a.scal[IADMM_S_IRHO_IN], irho_eq = a.scal[IADMM_S_IRHO_EQ];
+  float col[NG * 4];
+#pragma unroll
+  for (int i = 0; i < NG * 4; ++i) col[i] = 0.f;
+  // pass A: dr = K dg  (t1 = Q dg1, t3 = A0 dg1, red = A0^T dg2)
+  sweep<NG, VEC, true, false>(Qb, n, n, us, nullptr, t1, col, wave, nw, lane);
+  if (m > 0) sweep<NG, VEC, true, true>(Ab, m, n, us, ws, t3, col, wave, nw, lane);
+  col_reduce<NG, VEC>(col, red, n, wave, nw, lane);
+  float ds = 0.f;
+  for (int i = tid; i < n; i += blockDim.x) us[i] = ((t1[i] + sigma * us[i]) + red[i]);  // dr1
+  for (int j = tid; j < m; j += blockDim.x) {
+    const bool ineq = j < a.num_ineq;
+    const float rho = ineq ? rho_in : rho_eq, iota = ineq ? irho_in : irho_eq;
+    const float kappa = ineq ? 1.f : 1e3f;
+    const float dg2 = ws[j];
+    const float dr2 = t3[j] + (-iota) * dg2;
+    const float r2 = a.r[b * N + n + j];
+    const float diota = -dg2 * r2 + dr2 * (a.y[b * m + j] - a.xv[b * N + n + j]);
+    ds += kappa * (-diota / (rho * rho));
+    ws[j] = dr2;
+  }
+  __syncthreads();
+  // pass B: K^T dr  (red = Q^T dr1 + A0^T dr2, t3 = A0 dr1)
+#pragma unroll
+  for (int i = 0; i < NG * 4; ++i) col[i] = 0.f;
+  sweep<NG, VEC, false, true>(Qb, n, n, nullptr, us, nullptr, col, wave, nw, lane);
+  if (m > 0) sweep<NG, VEC, true, true>(Ab, m, n, us, ws, t3, col, wave, nw, lane);
+  col_reduce<NG, VEC>(col, red, n, wave, nw, lane);
+  for (int i = tid; i < n; i += blockDim.x) {
+    a.dxv[b * N + i] += red[i] + sigma * us[i];
+    a.dx[b * n + i] += -sigma * us[i];
+  }
+  for (int j = tid; j < m; j += blockDim.x) {
+    const float iota = j < a.num_ineq ? irho_in : irho_eq;
+    a.dxv[b * N + n + j] += t3[j] + (-iota) * ws[j];
+    a.dz[b * m + j] += -ws[j];
+    a.dy[b * m + j] += iota * ws[j];
+  }
+  const float s = block_sum(ds, red);
+  if (tid == 0) a.ds_inst[b] = s;
+}
+
+// ------------------------------------------------------------------ schedule backward
+// drho[t] += s(1-s) * (sum of ds partials), dalpha[t] += 2 sig(a)(1-sig(a)) * sum da, db_h += sum dbh
+__global__ void sched_bwd_kernel(const float* rho_param, const float* alpha_param, int64_t t,
+                                 const float* upd_partials, int nblk, const float* kkt_ds, int64_t B,
+                                 float* drho, float* dalpha, float* dbh) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  float ds = 0.f, da = 0.f, db = 0.f;
+  for (int k = 0; k < nblk; ++k) {
+    ds += upd_partials[4 * k + 0];
+    da += upd_partials[4 * k + 1];
+    db += upd_partials[4 * k + 2];
+  }
+  for (int64_t b = 0; b < B; ++b) ds += kkt_ds[b];
+  const float s = sigmoidf_(rho_param[t]);
+  const float sa = sigmoidf_(alpha_param[t]);
+  drho[t] += ds * s * (1.f - s);
+  dalpha[t] += da * 2.f * sa * (1.f - sa);
+  dbh[0] += db;
+}
+
+// ------------------------------------------------------------------ loss + gradient
+struct LossArgs {
+  int n, m;
+  const float *Q, *p, *A0, *x, *y, *z, *cp, *cd;   // cp/cd: per-instance upstream coefficients
+  float *primal, *dual, *dx, *dy, *dz;
+};
+
+// primal = ||A0 x - z||, dual = ||Q x + p + A0^T y||; dx = cp A0^T ep^ + cd Q^T ed^,
+// dz = -cp ep^, dy = cd A0 ed^  (e^ = e/||e||, 0 when ||e|| = 0, like torch's norm backward)
+template <int NG, bool VEC>
+__global__ __launch_bounds__(256) void loss_grad_kernel(LossArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  const int n = a.n, m = a.m;
+  float* xs = sm;        // n : x -> ed^
+  float* ys = xs + n;    // m : y -> ep^
+  float* t1 = ys + m;    // n
+  float* t3 = t1 + n;    // m
+  float* red = t3 + m;   // n
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, nw = blockDim.x >> 6;
+  const size_t b = blockIdx.x;
+  const float* Qb = a.Q + b * n * n;
+  const float* Ab = a.A0 + b * m * n;
+  for (int i = tid; i < n; i += blockDim.x) xs[i] = a.x[b * n + i];
+  for (int j = tid; j < m; j += blockDim.x) ys[j] = a.y[b * m + j];
+  __syncthreads();
+  float col[NG * 4];
+#pragma unroll
+  for (int i = 0; i < NG * 4; ++i) col[i] = 0.f;
+  sweep<NG, VEC, true, false>(Qb, n, n, xs, nullptr, t1, col, wave, nw, lane);
+  if (m > 0) sweep<NG, VEC, true, true>(Ab, m, n, xs, ys, t3, col, wave, nw, lane);
+  col_reduce<NG, VEC>(col, red, n, wave, nw, lane);
+  float dd = 0.f, pp = 0.f;
+  for (int i = tid; i < n; i += blockDim.x) {
+    const float e = (t1[i] + a.p[b * n + i]) + red[i];
+    t1[i] = e;
+    dd = fmaf(e, e, dd);
+  }
+  for (int j = tid; j < m; j += blockDim.x) {
+    const float e = t3[j] - a.z[b * m + j];
+    t3[j] = e;
+    pp = fmaf(e, e, pp);
+  }
+  const float nd = sqrtf(block_sum(dd, red));
+  const float np = sqrtf(block_sum(pp, red));
+  const float cp = a.cp ? a.cp[b] : 0.f, cd = a.cd ? a.cd[b] : 0.f;
+  const float sd = nd > 0.f ? cd / nd : 0.f, sp = np > 0.f ? cp / np : 0.f;
+  for (int i = tid; i < n; i += blockDim.x) xs[i] = t1[i];  // ed
+  for (int j = tid; j < m; j += blockDim.x) {
+    ys[j] = t3[j];                                           // ep
+    if (a.dz) a.dz[b * m + j] = -sp * t3[j];
+  }
+  __syncthreads();
+  // pass 2: red = Q^T ed (x sd) + A0^T ep (x sp) ; t3 = A0 ed
+#pragma unroll
+  for (int i = 0; i < NG * 4; ++i) col[i] = 0.f;
+  sweep<NG, VEC, false, true>(Qb, n, n, nullptr, xs, nullptr, col, wave, nw, lane);
+  float cola[NG * 4];
+#pragma unroll
+  for (int i = 0; i < NG * 4; ++i) cola[i] = 0.f;
+  if (m > 0) sweep<NG, VEC, true, true>(Ab, m, n, xs, ys, t3, cola, wave, nw, lane);
+#pragma unroll
+  for (int i = 0; i < NG * 4; ++i) col[i] = sd * col[i] + sp * cola[i];
+  col_reduce<NG, VEC>(col, red, n, wave, nw, lane);
+  for (int i = tid; i < n; i += blockDim.x) if (a.dx) a.dx[b * n + i] = red[i];
+  for (int j = tid; j < m; j += blockDim.x) if (a.dy) a.dy[b * m + j] = sd * t3[j];
+  if (tid == 0) {
+    if (a.primal) a.primal[b] = np;
+    if (a.dual) a.dual[b] = nd;
+  }
+}
+
+}  // namespace iadmm
+
+using namespace iadmm;
+
+extern "C" int iadmm_admm_update_bwd(int64_t B, int64_t n, int64_t m, int64_t num_ineq, const float* x,
+                                     const float* y, const float* z, const float* xv_out, const float* zl,
+                                     const float* zu, const float* scal, const float* dx_out,
+                                     const float* dy_out, const float* dz_out, const float* dxv_out,
+                                     float* dx, float* dy, float* dz, float* dxv, float* dq,
+                                     float* partials, int64_t nblocks, void* stream) {
+  if (B <= 0 || n <= 0 || m < 0 || num_ineq < 0 || num_ineq > m || nblocks <= 0 || nblocks > 65535) return IADMM_E_ARG;
+  if (!x || !xv_out || !scal || !dx || !dxv || !dq || !partials) return IADMM_E_ARG;
+  if (m > 0 && (!y || !z || !zl || !zu || !dy || !dz)) return IADMM_E_ARG;
+  UpdBwdArgs a{B, (int)n, (int)m, (int)num_ineq, x, y, z, xv_out, zl, zu, scal, dx_out, dy_out, dz_out, dxv_out,
+               dx, dy, dz, dxv, dq, partials};
+  hipLaunchKernelGGL(admm_update_bwd_kernel, dim3((unsigned)nblocks), dim3(256), 0, (hipStream_t)stream, a);
+  IADMM_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int iadmm_lstm_cell_bwd(int64_t M, int64_t h, const float* H, const float* C, const float* xv,
+                                   const float* g, const float* Upk, const float* Wx, const float* dq,
+                                   const float* dHn, const float* dCn, float* dC, float* dP, float* whslab,
+                                   float* inpart, void* stream) {
+  if (M <= 0 || h <= 0 || !H || !C || !xv || !g || !Upk || !Wx || !dq || !dC || !dP || !whslab || !inpart)
+    return IADMM_E_ARG;
+  const int64_t nrt = (M + kRows - 1) / kRows, njt = (h + kJT - 1) / kJT;
+  if (nrt * njt > 0x7fffffffLL || h > (1 << 16)) return IADMM_E_SIZE;
+  CellBwdArgs a{M, (int)h, (int)njt, (int)((h + kBK - 1) / kBK), (int)nrt, H, C, xv, g, Upk, Wx, dq, dHn, dCn,
+                dC, dP, whslab, inpart};
+  const bool vec = (h % 4 == 0) && aligned16(H);
+  const dim3 grid((unsigned)(nrt * njt));
+  if (vec) hipLaunchKernelGGL(lstm_cell_bwd_kernel<true>, grid, dim3(256), 0, (hipStream_t)stream, a);
+  else hipLaunchKernelGGL(lstm_cell_bwd_kernel<false>, grid, dim3(256), 0, (hipStream_t)stream, a);
+  IADMM_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int iadmm_in_reduce(int64_t M, int64_t njt, const float* inpart, float* dxv, float* dg, void* stream) {
+  if (M <= 0 || njt <= 0 || !inpart || !dxv || !dg) return IADMM_E_ARG;
+  const int64_t blocks = (M + 255) / 256;
+  hipLaunchKernelGGL(in_reduce_kernel, dim3((unsigned)(blocks < 8192 ? blocks : 8192)), dim3(256), 0,
+                     (hipStream_t)stream, M, (int)njt, inpart, dxv, dg);
+  IADMM_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int iadmm_kkt_bwd(int64_t B, int64_t n, int64_t m, int64_t num_ineq, const float* Q, const float* A0,
+                             const float* xv, const float* y, const float* r, const float* dg, float sigma,
+                             const float* scal, float* dxv, float* dx, float* dy, float* dz, float* ds_inst,
+                             void* stream) {
+  if (B <= 0 || n <= 0 || m < 0 || num_ineq < 0 || num_ineq > m) return IADMM_E_ARG;
+  if (!Q || !xv || !r || !dg || !scal || !dxv || !dx || !ds_inst || (m > 0 && (!A0 || !y || !dy || !dz)))
+    return IADMM_E_ARG;
+  if (3 * n + 2 * m > 40960 || B > 0x7fffffff) return IADMM_E_SIZE;
+  KktBwdArgs a{(int)n, (int)m, (int)num_ineq, Q, A0, xv, y, r, dg, sigma, scal, dxv, dx, dy, dz, ds_inst};
+  const int ng = ng_for(n);
+  const bool vec = (n % 4 == 0) && aligned16(Q) && (m == 0 || aligned16(A0));
+  const size_t lds = (3 * n + 2 * m) * sizeof(float);
+  IADMM_DISPATCH_NG(ng, vec, {
+    hipLaunchKernelGGL((kkt_bwd_kernel<NG_, V_>), dim3((unsigned)B), dim3(256), lds, (hipStream_t)stream, a);
+  });
+  IADMM_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int iadmm_sched_bwd(const float* rho_param, const float* alpha_param, int64_t t,
+                               const float* upd_partials, int64_t nblk, const float* kkt_ds, int64_t B,
+                               float* drho, float* dalpha, float* dbh, void* stream) {
+  if (!rho_param || !alpha_param || !upd_partials || !kkt_ds || !drho || !dalpha || !dbh || t < 0) return IADMM_E_ARG;
+  hipLaunchKernelGGL(sched_bwd_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, rho_param, alpha_param, t,
+                     upd_partials, (int)nblk, kkt_ds, B, drho, dalpha, dbh);
+  IADMM_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int iadmm_loss_grad(int64_t B, int64_t n, int64_t m, const float* Q, const float* p, const float* A0,
+                               const float* x, const float* y, const float* z, const float* cp, const float* cd,
+                               float* primal, float* dual, float* dx, float* dy, float* dz, void* stream) {
+  if (B <= 0 || n <= 0 || m < 0 || !Q || !p || !x || (m > 0 && (!A0 || !y || !z))) return IADMM_E_ARG;
+  if (3 * n + 2 * m > 40960 || B > 0x7fffffff) return IADMM_E_SIZE;
+  LossArgs a{(int)n, (int)m, Q, p, A0, x, y, z, cp, cd, primal, dual, dx, dy, dz};
+  const int ng = ng_for(n);
+  const bool vec = (n % 4 == 0) && aligned16(Q) && (m == 0 || aligned16(A0));
+  const size_t lds = (3 * n + 2 * m) * sizeof(float);
+  IADMM_DISPATCH_NG(ng, vec, {
+    hipLaunchKernelGGL((loss_grad_kernel<NG_, V_>), dim3((unsigned)B), dim3(256), lds, (hipStream_t)stream, a);
+  });
+  IADMM_CHECK_LAUNCH();
+  return 0;
+}

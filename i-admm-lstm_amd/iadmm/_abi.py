@@ -18,7 +18,7 @@ SIGNATURES = {
     "iadmm_version": (cint, []),
     "iadmm_schedule": (cint, [vp, vp, i64, vp, vp]),
     "iadmm_schedule_fixed_alpha": (cint, [vp, f32, vp, vp]),
-    "iadmm_kkt_resgrad": (cint, [i64, i64, i64, i64, vp, vp, vp, vp, vp, vp, vp, f32, vp, vp, vp, vp, vp]),
+    "iadmm_kkt_resgrad": (cint, [i64, i64, i64, i64, vp, vp, vp, vp, vp, vp, vp, f32, vp, vp, vp, vp, vp, vp]),
     "iadmm_kkt_lsres": (cint, [i64, i64, i64, i64, vp, vp, vp, vp, vp, vp, vp, f32, vp, vp, vp]),
     "iadmm_lstm_packed_floats": (i64, [i64]),
     "iadmm_lstm_wx_floats": (i64, [i64]),
@@ -36,6 +36,16 @@ SIGNATURES = {
     "iadmm_kkt_assemble": (cint, [i64, i64, i64, i64, vp, vp, f32, vp, vp, vp, vp]),
     "iadmm_kkt_rhs": (cint, [i64, i64, i64, i64, vp, vp, vp, vp, f32, vp, vp, vp, vp]),
     "iadmm_kkt_matvec": (cint, [i64, i64, i64, i64, vp, vp, vp, f32, vp, vp, cint, vp, vp]),
+    "iadmm_gemm_nt": (cint, [i64, i64, i64, vp, vp, vp, cint, vp]),
+    "iadmm_gemm_tn_splits": (i64, [i64, i64]),
+    "iadmm_gemm_tn": (cint, [i64, i64, i64, i64, vp, vp, vp, vp, cint, vp]),
+    "iadmm_slab_reduce": (cint, [i64, i64, vp, vp, cint, vp]),
+    "iadmm_admm_update_bwd": (cint, [i64, i64, i64, i64] + [vp] * 17 + [i64, vp]),
+    "iadmm_lstm_cell_bwd": (cint, [i64, i64] + [vp] * 13 + [vp]),
+    "iadmm_in_reduce": (cint, [i64, i64, vp, vp, vp, vp]),
+    "iadmm_kkt_bwd": (cint, [i64, i64, i64, i64, vp, vp, vp, vp, vp, vp, f32, vp, vp, vp, vp, vp, vp, vp]),
+    "iadmm_sched_bwd": (cint, [vp, vp, i64, vp, i64, vp, i64, vp, vp, vp, vp]),
+    "iadmm_loss_grad": (cint, [i64, i64, i64] + [vp] * 13 + [vp]),
 }
 
 ERRORS = {-1: "bad argument", -2: "size beyond kernel limit", -3: "misaligned pointer"}

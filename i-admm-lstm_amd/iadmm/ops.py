@@ -54,13 +54,14 @@ def schedule_fixed_alpha(scal, alpha, out=None):
 
 
 # --------------------------------------------------------------------------- KKT
-def kkt_resgrad(Q, A0, p, x, y, z, xv, sigma, scal, num_ineq, g=None, btild=None, rho_vec=None):
+def kkt_resgrad(Q, A0, p, x, y, z, xv, sigma, scal, num_ineq, g=None, btild=None, rho_vec=None,
+                r_out=None):
     """g = K^T (K xv - b~) with the implicit KKT matrix (models/lstm.py:67-72)."""
     B, n = Q.shape[0], Q.shape[1]
     m = A0.shape[1]
     g = empty(B, n + m, like=Q) if g is None else g
     _abi.call("iadmm_kkt_resgrad", B, n, m, int(num_ineq), _p(Q), _p(A0), _p(p), _p(x), _p(y), _p(z),
-              _p(xv), float(sigma), _p(scal), _p(g), _p(btild), _p(rho_vec), _stream())
+              _p(xv), float(sigma), _p(scal), _p(g), _p(btild), _p(rho_vec), _p(r_out), _stream())
     return g
 
 
@@ -214,3 +215,94 @@ def lu_solve(LU, piv, b):
         raise TypeError("piv must be contiguous int32")
     _abi.call("iadmm_lu_solve", B, N, _p(LU), piv.data_ptr(), _p(x), _stream())
     return x
+
+
+# --------------------------------------------------------------------------- training backward
+def gemm_nt(X, W, out=None, accumulate=False):
+    """out[M,Ni] (+)= X[M,K] W[Ni,K]^T."""
+    M, K = X.shape
+    Ni = W.shape[0]
+    out = empty(M, Ni, like=X) if out is None else out
+    _abi.call("iadmm_gemm_nt", M, Ni, K, _p(X), _p(W), _p(out), int(bool(accumulate)), _stream())
+    return out
+
+
+def gemm_tn(X, Y, rows_per_split=4096, out=None, accumulate=False):
+    """out[Ni,No] (+)= X[M,Ni]^T Y[M,No] (split over M, fixed-order reduction)."""
+    M, Ni = X.shape
+    No = Y.shape[1]
+    ns = int(_abi.lib().iadmm_gemm_tn_splits(M, rows_per_split))
+    slab = empty(ns, Ni, No, like=X)
+    out = empty(Ni, No, like=X) if out is None else out
+    _abi.call("iadmm_gemm_tn", M, Ni, No, rows_per_split, _p(X), _p(Y), _p(slab), _p(out),
+              int(bool(accumulate)), _stream())
+    return out
+
+
+def slab_reduce(slab, out=None, accumulate=False):
+    ns = slab.shape[0]
+    nelem = slab[0].numel()
+    out = empty(*slab.shape[1:], like=slab) if out is None else out
+    _abi.call("iadmm_slab_reduce", nelem, ns, _p(slab), _p(out), int(bool(accumulate)), _stream())
+    return out
+
+
+UPD_BWD_BLOCKS = 256
+
+
+def admm_update_bwd(n, m, num_ineq, x, y, z, xv_out, zl, zu, scal, dx_o, dy_o, dz_o, dxv_o):
+    B = x.shape[0]
+    dx, dy, dz = torch.empty_like(x), torch.empty_like(y), torch.empty_like(z)
+    dxv, dq = torch.empty_like(xv_out), torch.empty_like(xv_out)
+    partials = empty(UPD_BWD_BLOCKS, 4, like=x)
+    _abi.call("iadmm_admm_update_bwd", B, n, m, int(num_ineq), _p(x), _p(y), _p(z), _p(xv_out), _p(zl), _p(zu),
+              _p(scal), _p(dx_o), _p(dy_o), _p(dz_o), _p(dxv_o), _p(dx), _p(dy), _p(dz), _p(dxv), _p(dq),
+              _p(partials), UPD_BWD_BLOCKS, _stream())
+    return dx, dy, dz, dxv, dq, partials
+
+
+def lstm_cell_bwd(H, C, xv, g, Upk, Wx, dq, dHn=None, dCn=None):
+    h = H.shape[-1]
+    M = H.numel() // h
+    nrt, ntl = (M + 255) // 256, lstm_ntiles(h)
+    dC = torch.empty_like(C)
+    dP = empty(M, 4 * h, like=H)
+    whslab = empty(nrt, h, like=H)
+    inpart = empty(ntl, M, 2, like=H)
+    _abi.call("iadmm_lstm_cell_bwd", M, h, _p(H), _p(C), _p(xv), _p(g), _p(Upk), _p(Wx), _p(dq), _p(dHn), _p(dCn),
+              _p(dC), _p(dP), _p(whslab), _p(inpart), _stream())
+    return dC, dP, whslab, inpart
+
+
+def in_reduce(inpart, dxv, dg=None):
+    ntl, M = inpart.shape[0], inpart.shape[1]
+    dg = empty(M, like=inpart) if dg is None else dg
+    _abi.call("iadmm_in_reduce", M, ntl, _p(inpart), _p(dxv), _p(dg), _stream())
+    return dg
+
+
+def kkt_bwd(Q, A0, xv, y, r, dg, sigma, scal, num_ineq, dxv, dx, dy, dz):
+    B, n = Q.shape[0], Q.shape[1]
+    m = A0.shape[1]
+    ds = empty(B, like=Q)
+    _abi.call("iadmm_kkt_bwd", B, n, m, int(num_ineq), _p(Q), _p(A0), _p(xv), _p(y), _p(r), _p(dg), float(sigma),
+              _p(scal), _p(dxv), _p(dx), _p(dy), _p(dz), _p(ds), _stream())
+    return ds
+
+
+def sched_bwd(rho_param, alpha_param, t, upd_partials, kkt_ds, drho, dalpha, dbh):
+    _abi.call("iadmm_sched_bwd", _p(rho_param), _p(alpha_param), int(t), _p(upd_partials), upd_partials.shape[0],
+              _p(kkt_ds), kkt_ds.shape[0], _p(drho), _p(dalpha), _p(dbh), _stream())
+
+
+def loss_grad(Q, p, A0, x, y, z, cp=None, cd=None, want_grad=True):
+    """(primal[B], dual[B], dx, dy, dz) of utils.py:68-71 with upstream coefficients cp, cd [B]."""
+    B, n = Q.shape[0], Q.shape[1]
+    m = A0.shape[1]
+    pr, du = empty(B, like=Q), empty(B, like=Q)
+    dx = dy = dz = None
+    if want_grad:
+        dx, dy, dz = empty(B, n, like=Q), empty(B, m, like=Q), empty(B, m, like=Q)
+    _abi.call("iadmm_loss_grad", B, n, m, _p(Q), _p(p), _p(A0), _p(x), _p(y), _p(z), _p(cp), _p(cd), _p(pr), _p(du),
+              _p(dx), _p(dy), _p(dz), _stream())
+    return pr, du, dx, dy, dz

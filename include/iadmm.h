@@ -63,14 +63,15 @@ int iadmm_schedule_fixed_alpha(const float* scal_in, float alpha, float* scal_ou
  * K materialisation, the RHS and the two dependent bmm).  K is never formed:
  *   K = [[Q + sigma I, A0^T], [A0, -diag(1/rho_vec)]],  b~ = [sigma x - p ; z - y / rho_vec].
  * Q[B,n,n], A0[B,m,n], p/x[B,n], y/z[B,m], xv[B,n+m] -> g[B,n+m];
- * btild[B,n+m] and rho_vec[B,m] are optional outputs (may be NULL).
+ * btild[B,n+m], rho_vec[B,m] and r_out[B,n+m] (= K xv - b~, kept for the training backward)
+ * are optional outputs (may be NULL).
  * Rows [0,num_ineq) of A0 use rho_in, rows [num_ineq,m) rho_eq.
  * Limit: 3n + 2m <= 40960 (on-chip vectors). */
 int iadmm_kkt_resgrad(int64_t B, int64_t n, int64_t m, int64_t num_ineq,
                       const float* Q, const float* A0, const float* p,
                       const float* x, const float* y, const float* z, const float* xv,
                       float sigma, const float* scal,
-                      float* g, float* btild, float* rho_vec, void* stream);
+                      float* g, float* btild, float* rho_vec, float* r_out, void* stream);
 
 /* ||K xv - b~||_2 per instance (main.py:952 ``ls_res``), same implicit K. out[B]. */
 int iadmm_kkt_lsres(int64_t B, int64_t n, int64_t m, int64_t num_ineq,
@@ -173,6 +174,70 @@ int iadmm_metrics(int64_t B, int64_t n, int64_t m, const float* Q, const float* 
  * M[B,R,C], x[B,C], rhs[B,R] (unused for mode 0).  Limit: R + C <= 40960. */
 int iadmm_bmv(int64_t B, int64_t R, int64_t C, const float* M, const float* x, const float* rhs,
               int mode, float* out, void* stream);
+
+/* ------------------------------------------------------------------------------------------
+ * Training backward (autograd through models/lstm.py:47-96 and utils.py:68-71; main.py:336-358).
+ * All reductions are fixed-order partial slabs: gradients are bitwise reproducible.
+ * ---------------------------------------------------------------------------------------- */
+
+/* out[M,Ni] (+)= X[M,K] . W[Ni,K]^T on fp32 MFMA (dH = dP . U_cat^T). */
+int iadmm_gemm_nt(int64_t M, int64_t Ni, int64_t K, const float* X, const float* W, float* out,
+                  int accumulate, void* stream);
+
+/* out[Ni,No] (+)= X[M,Ni]^T . Y[M,No], split over M in slices of rows_per_split (multiple of 32):
+ * slab[iadmm_gemm_tn_splits(M, rows_per_split)][Ni][No] is caller-owned scratch. */
+int64_t iadmm_gemm_tn_splits(int64_t M, int64_t rows_per_split);
+int iadmm_gemm_tn(int64_t M, int64_t Ni, int64_t No, int64_t rows_per_split, const float* X,
+                  const float* Y, float* slab, float* out, int accumulate, void* stream);
+
+/* out[e] (+)= sum_s slab[s][e], s < nsplit, fixed order. */
+int iadmm_slab_reduce(int64_t nelem, int64_t nsplit, const float* slab, float* out, int accumulate,
+                      void* stream);
+
+/* Backward of iadmm_admm_update (Stage I form): adjoints dx_out/dy_out/dz_out/dxv_out of
+ * (x', y', z', xv') (NULL = 0) -> dx, dy, dz (written), dxv (written, pass-through), dq = -dxv
+ * (adjoint of the projection q = H'W_h + b_h) and per-block partials[nblocks][4] =
+ * (d s, d alpha-scalar a, d b_h, 0) for iadmm_sched_bwd. */
+int iadmm_admm_update_bwd(int64_t B, int64_t n, int64_t m, int64_t num_ineq, const float* x,
+                          const float* y, const float* z, const float* xv_out, const float* zl,
+                          const float* zu, const float* scal, const float* dx_out,
+                          const float* dy_out, const float* dz_out, const float* dxv_out,
+                          float* dx, float* dy, float* dz, float* dxv, float* dq,
+                          float* partials, int64_t nblocks, void* stream);
+
+/* Backward of iadmm_lstm_cell_fwd: recomputes the gates (fp32 MFMA), consumes dq[M] and the
+ * adjoints dHn, dCn [M,h] of H', C' (NULL = 0) and writes dC [M,h] (may alias dCn),
+ * dP [M][4h] (gate pre-activation adjoints, gate-major columns g*h + j),
+ * whslab [ceil(M/256)][h] (per-row-tile sums of H' dq, reduce -> dW_h) and
+ * inpart [ntiles][M][2] (per-hidden-tile sums of dP W^T, reduce with iadmm_in_reduce). */
+int iadmm_lstm_cell_bwd(int64_t M, int64_t h, const float* H, const float* C, const float* xv,
+                        const float* g, const float* Upk, const float* Wx, const float* dq,
+                        const float* dHn, const float* dCn, float* dC, float* dP, float* whslab,
+                        float* inpart, void* stream);
+
+/* dxv[R] += sum_t inpart[t][R][0] ; dg[R] = sum_t inpart[t][R][1]. */
+int iadmm_in_reduce(int64_t M, int64_t ntiles, const float* inpart, float* dxv, float* dg,
+                    void* stream);
+
+/* Backward of iadmm_kkt_resgrad given dg: dr = K dg, dxv += K^T dr, dx += -sigma dr1,
+ * dz += -dr2, dy += dr2 / rho, ds_inst[B] = this instance's d s through 1/rho (r = saved r_out). */
+int iadmm_kkt_bwd(int64_t B, int64_t n, int64_t m, int64_t num_ineq, const float* Q,
+                  const float* A0, const float* xv, const float* y, const float* r, const float* dg,
+                  float sigma, const float* scal, float* dxv, float* dx, float* dy, float* dz,
+                  float* ds_inst, void* stream);
+
+/* drho[t] += s(1-s) sum(ds), dalpha[t] += 2 sig(alpha_t)(1-sig(alpha_t)) sum(da), dbh += sum(db). */
+int iadmm_sched_bwd(const float* rho_param, const float* alpha_param, int64_t t,
+                    const float* upd_partials, int64_t nblk, const float* kkt_ds, int64_t B,
+                    float* drho, float* dalpha, float* dbh, void* stream);
+
+/* Loss of utils.py:68-71 and its gradient: primal[B] = ||A0 x - z||, dual[B] = ||Qx + p + A0^T y||,
+ * dx = cp A0^T e_p/|e_p| + cd Q^T e_d/|e_d|, dy = cd A0 e_d/|e_d|, dz = -cp e_p/|e_p| with
+ * per-instance upstream coefficients cp[B], cd[B] (any output may be NULL). */
+int iadmm_loss_grad(int64_t B, int64_t n, int64_t m, const float* Q, const float* p,
+                    const float* A0, const float* x, const float* y, const float* z,
+                    const float* cp, const float* cd, float* primal, float* dual, float* dx,
+                    float* dy, float* dz, void* stream);
 
 #ifdef __cplusplus
 }

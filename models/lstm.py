@@ -8,7 +8,8 @@ runs three gfx950 kernels through libiadmm.so:
   iadmm_admm_update   xv / x / z / y updates                         (lstm.py:80-94)
 ``A_tild`` comes back as a lazy :class:`iadmm.kktop.KKTOperator` (``torch.bmm(A_tild, xv)``
 works; ``.dense()`` materialises K).  Outputs are fresh tensors (functional semantics): the
-caller may keep its inputs.
+caller may keep its inputs.  Under grad mode the call goes through
+:class:`iadmm.autograd.IterationFn`, whose backward is a set of HIP kernels (training).
 """
 import torch
 import torch.nn as nn
@@ -16,7 +17,8 @@ import torch.nn as nn
 import iadmm_path  # noqa: F401
 from iadmm import ops
 from iadmm.kktop import KKTOperator
-from iadmm.solver import PackedWeights, param_dict
+from iadmm.autograd import IterationFn
+from iadmm.solver import PARAM_NAMES, PackedWeights, param_dict
 
 _GATES = ("i", "f", "o", "u")
 
@@ -55,10 +57,6 @@ class LSTM(nn.Module):
         return "lstm"
 
     def forward(self, t, num_ineq, num_eq, x, y, z, xv, sigma, H_t, C_t, **kwargs):
-        if torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters()):
-            raise NotImplementedError(
-                "autograd through the HIP I-ADMM-LSTM cell is not built yet (training backward "
-                "kernels are the next milestone); run inference under torch.no_grad()")
         Q, p, A0, zl, zu = (kwargs[k] for k in ("Q", "p", "A0", "zl", "zu"))
         B, n = x.shape[0], x.shape[1]
         m = y.shape[1]
@@ -73,6 +71,9 @@ class LSTM(nn.Module):
         yv, zvv = c(y).reshape(B, m), c(z).reshape(B, m)
         zlv, zuv = c(zl).reshape(B, m), c(zu).reshape(B, m)
         params = param_dict(self)
+        if torch.is_grad_enabled() and (any(v.requires_grad for v in params.values()) or any(
+                isinstance(v, torch.Tensor) and v.requires_grad for v in (x, y, z, xv, H_t, C_t))):
+            return self._forward_autograd(t, num_ineq, sigma, x, y, z, xv, H_t, C_t, Q, pv, A0, zlv, zuv, params)
 
         scal = ops.schedule(c(self.rho), c(self.alpha), t)
         btild = ops.empty(B, N, like=Q)
@@ -83,5 +84,21 @@ class LSTM(nn.Module):
         Hn, Cn, part = ops.lstm_cell(c(H_t), c(C_t), xv2, g, Upk, Wx)
         xvo, xo, yo, zo = ops.admm_update(n, m, num_ineq, part, c(self.b_h), xv2, xv_, yv, zvv, zlv, zuv, scal)
         A_tild = KKTOperator(Q, A0, sigma, scal, num_ineq)
+        return (xo.unsqueeze(-1), yo.unsqueeze(-1), zo.unsqueeze(-1), xvo.unsqueeze(-1), Hn, Cn,
+                A_tild, btild.unsqueeze(-1), rho_vec.unsqueeze(-1))
+
+    def _forward_autograd(self, t, num_ineq, sigma, x, y, z, xv, H_t, C_t, Q, pv, A0, zlv, zuv, params):
+        """Training path: the same kernels wrapped in iadmm.autograd.IterationFn, whose backward
+        runs the HIP backward kernels (TBPTT through main.py:336-350)."""
+        B, n = x.shape[0], x.shape[1]
+        m = y.shape[1]
+        N = n + m
+        flat = lambda a, k: a.float().reshape(B, k).contiguous()  # noqa: E731 (keeps autograd)
+        meta = (int(t), int(num_ineq), float(sigma), (Q, pv, A0, zlv, zuv), self._packed)
+        xo, yo, zo, xvo, Hn, Cn, btild, rho_vec = IterationFn.apply(
+            meta, flat(x, n), flat(y, m), flat(z, m), flat(xv, N), H_t.float().contiguous(),
+            C_t.float().contiguous(), *[params[k] for k in PARAM_NAMES])
+        A_tild = KKTOperator(Q, A0, sigma, ops.schedule(self.rho.detach().contiguous(),
+                                                        self.alpha.detach().contiguous(), t), num_ineq)
         return (xo.unsqueeze(-1), yo.unsqueeze(-1), zo.unsqueeze(-1), xvo.unsqueeze(-1), Hn, Cn,
                 A_tild, btild.unsqueeze(-1), rho_vec.unsqueeze(-1))

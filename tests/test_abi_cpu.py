@@ -45,8 +45,8 @@ def test_size_queries_without_gpu():
 def test_bad_arguments_rejected_before_launch():
     # argument checks run on the host before any HIP call: safe without a GPU
     with pytest.raises(_abi.IadmmError, match="bad argument"):
-        _abi.call("iadmm_kkt_resgrad", 0, 10, 10, 5, *([None] * 7), 1.0, None, None, None, None, None)
+        _abi.call("iadmm_kkt_resgrad", 0, 10, 10, 5, *([None] * 7), 1.0, None, None, None, None, None, None)
     with pytest.raises(_abi.IadmmError, match="size beyond"):
-        _abi.call("iadmm_kkt_resgrad", 1, 20000, 20000, 0, *([1] * 7), 1.0, 1, 1, None, None, None)
+        _abi.call("iadmm_kkt_resgrad", 1, 20000, 20000, 0, *([1] * 7), 1.0, 1, 1, None, None, None, None)
     with pytest.raises(_abi.IadmmError, match="bad argument"):
         _abi.call("iadmm_lstm_cell_fwd", 10, 8, 16, 16, 16, 16, 16, 16, 16, 16, 16, None)

@@ -1,0 +1,77 @@
+"""Training (row a12) on the GPU: gradients of the reference's TBPTT loss (main.py:336-350)
+through the HIP forward + backward kernels against the gradients the reference itself produced
+(tests/golden, autograd on the PyTorch-CPU reference).
+
+Tolerance: rel-L2 per parameter <= 2e-3 (summation-order noise of fp32 forward and backward
+accumulated over T unrolled iterations); the loss value <= 1e-4."""
+import numpy as np
+import pytest
+import torch
+
+import iadmm_path  # noqa: F401
+
+pytestmark = pytest.mark.gpu
+
+
+def rel_l2(a, b):
+    a = torch.as_tensor(a).double().cpu()
+    b = torch.as_tensor(b).double().cpu()
+    return float((a - b).norm() / max(b.norm(), 1e-30))
+
+
+def test_grads_match_reference(golden):
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    name, g = golden
+    if "train_loss" not in g:
+        pytest.skip("no gradient fixture")
+    from models.lstm import LSTM
+    import utils
+    n, mi, me, h, T, B, scaling, _ = (int(v) for v in g["meta"])
+    m = mi + me
+    model = LSTM(m, 2, h, T, "cuda")
+    model.load_state_dict({k[len("param_"):]: torch.from_numpy(g[k]) for k in g if k.startswith("param_")})
+    model.train()
+    dev = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()  # noqa: E731
+    Q, p, A0, zl, zu = (dev(g["sc_" + k]) for k in ("Q", "p", "A0", "zl", "zu"))
+    x, y, z = torch.zeros(B, n, 1, device="cuda"), torch.zeros(B, m, 1, device="cuda"), torch.zeros(B, m, 1, device="cuda")
+    xv = torch.zeros(B, n + m, 1, device="cuda")
+    H, C = torch.zeros(B, n + m, h, device="cuda"), torch.zeros(B, n + m, h, device="cuda")
+    loss_tot = 0.0
+    for t in range(T):
+        x, y, z, xv, H, C, _, _, _ = model(t, mi, me, x, y, z, xv, float(g["sigma"]), H, C, Q=Q, p=p, A0=A0,
+                                           lb=None, ub=None, zl=zl, zu=zu)
+        _, _, loss = utils.primal_dual_loss(x, y, z, Q, p, A0)
+        loss_tot = loss_tot + loss.mean() / T
+    loss_tot.backward()
+    assert abs(loss_tot.item() - float(g["train_loss"])) <= 1e-4 * abs(float(g["train_loss"]))
+    bad = {}
+    for k, prm in model.named_parameters():
+        err = rel_l2(prm.grad, g["grad_" + k])
+        if err > 2e-3:
+            bad[k] = err
+    assert not bad, bad
+
+
+def test_loss_grad_matches_autograd():
+    """The loss kernel's gradient against torch autograd of the same formula (fp64)."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import utils
+    torch.manual_seed(0)
+    B, n, m = 3, 40, 24
+    Q = torch.randn(B, n, n, dtype=torch.float64)
+    p = torch.randn(B, n, 1, dtype=torch.float64)
+    A0 = torch.randn(B, m, n, dtype=torch.float64)
+    x = torch.randn(B, n, 1, dtype=torch.float64, requires_grad=True)
+    y = torch.randn(B, m, 1, dtype=torch.float64, requires_grad=True)
+    z = torch.randn(B, m, 1, dtype=torch.float64, requires_grad=True)
+    w = torch.tensor([0.3, 1.0, 2.0], dtype=torch.float64).reshape(B, 1, 1)
+    pr = torch.linalg.vector_norm(torch.bmm(A0, x) - z, dim=(1, 2), keepdim=True)
+    du = torch.linalg.vector_norm(torch.bmm(Q, x) + p + torch.bmm(A0.transpose(1, 2), y), dim=(1, 2), keepdim=True)
+    ((pr + 2 * du) * w).sum().backward()
+    xg, yg, zg = (v.detach().float().cuda().requires_grad_(True) for v in (x, y, z))
+    a, b_, _ = utils.primal_dual_loss(xg, yg, zg, Q.float().cuda(), p.float().cuda(), A0.float().cuda())
+    ((a + 2 * b_) * w.float().cuda()).sum().backward()
+    for mine, ref in ((xg, x), (yg, y), (zg, z)):
+        assert rel_l2(mine.grad, ref.grad) < 1e-5

@@ -93,9 +93,19 @@ def ub_dist(x, ub):
 
 
 def primal_dual_loss(x, y, z, Q, p, A0):
-    """(||A0 x - z||, ||Q x + p + A0^T y||, sum), each [B,1,1] (utils.py:68-71)."""
-    _no_grad_inputs(x, y, z, Q, p, A0)
+    """(||A0 x - z||, ||Q x + p + A0^T y||, sum), each [B,1,1] (utils.py:68-71).  Differentiable
+    in x, y, z (the training loss, main.py:346) through iadmm.autograd.LossFn."""
     B = x.shape[0]
+    if torch.is_grad_enabled() and any(t.requires_grad for t in (x, y, z)):
+        from iadmm.autograd import LossFn
+        _no_grad_inputs(Q, p, A0)
+        data = (Q.detach().float().contiguous(), p.detach().float().reshape(B, -1).contiguous(),
+                A0.detach().float().contiguous())
+        pr, du = LossFn.apply(x.float().reshape(B, -1).contiguous(), y.float().reshape(B, -1).contiguous(),
+                              z.float().reshape(B, -1).contiguous(), data)
+        pr, du = pr.reshape(B, 1, 1), du.reshape(B, 1, 1)
+        return pr, du, pr + du
+    _no_grad_inputs(x, y, z, Q, p, A0)
     _, pr, du = ops.metrics(Q.detach().float().contiguous(), _flat(p), A0.detach().float().contiguous(),
                             _flat(x), _flat(y), _flat(z))
     pr, du = pr.reshape(B, 1, 1), du.reshape(B, 1, 1)
