@@ -11,7 +11,11 @@ reads but never registers (main.py:191).  Implemented modes:
            "Parallel Time" and the optional ``--save_sol`` .mat file.  All compute runs in
            libiadmm.so kernels (iadmm/solver.py); per-iteration metrics stay on the device and
            are copied once per batch.
-  (train)  not built yet: training needs the backward kernels.
+  (train)  the training loop of main.py:187-547 for prob_type QP: Ruiz-scaled batches, TBPTT
+           windows through the HIP forward/backward kernels (iadmm/train.py), Adam, validation by
+           a full no-grad unroll, EarlyStopping checkpoints in the reference's .pth format.
+           One process per GPU under torch.distributed.run: each rank trains on its shard of
+           every batch and the gradients are all-reduced over RCCL (exact: the loss is a mean).
 """
 import argparse
 import gzip
@@ -53,6 +57,7 @@ def build_parser():
     add("--synthetic", action="store_true", help="generate instances instead of reading ./datasets")
     add("--random_init", action="store_true", help="random-init weights when no checkpoint exists")
     add("--data_dir", type=str, default="./datasets")
+    add("--micro_batch", type=int, default=0, help="instances per forward/backward pass (memory)")
     return p
 
 
@@ -176,11 +181,92 @@ def run_test(args):
     return reports, total_time
 
 
+def _instances(args, ids, device):
+    mi, me, n = args.num_ineq, args.num_eq, args.num_var
+    if args.synthetic:
+        parts = [qpdata.make_qp_batch(n, mi, me, 1, first_index=i, seed=args.seed, device=device) for i in ids]
+        d = {k: torch.cat([q[k] for q in parts]) for k in parts[0]}
+        d.update(G=d["A0"][:, :mi], A=d["A0"][:, mi:], c=d["zu"][:, :mi], b=d["zu"][:, mi:])
+        return d
+    return load_qp_instances(args, ids, device)
+
+
+def run_train(args):
+    """main.py:187-547 (QP): epochs of TBPTT batches + validation + EarlyStopping."""
+    from iadmm import parallel, train
+    from models.lstm import LSTM
+    from utils import EarlyStopping
+    if args.prob_type != "QP":
+        raise SystemExit(f"prob_type {args.prob_type!r} is out of scope (DESIGN.md §0); use QP")
+    world, rank, local = parallel.env()
+    device = f"cuda:{local}" if world > 1 else (args.device or "cuda:0")
+    torch.cuda.set_device(torch.device(device))
+    dist = parallel.init("nccl", local) if world > 1 else None
+    mi, me = args.num_ineq, args.num_eq
+    torch.manual_seed(args.seed)
+    model = LSTM(mi + me, args.input_dim, args.hidden_dim, args.outer_T, device)
+    save_path = os.path.join(args.save_dir, model.name(), "params", "QP_{}_{}_{}_{}_{}.pth".format(
+        args.num_var, args.num_ineq, args.num_eq, args.outer_T, args.hidden_dim))  # main.py:88-92
+    if rank == 0:
+        os.makedirs(os.path.dirname(save_path), exist_ok=True)
+    stopper = EarlyStopping(save_path, patience=args.patience)
+    optimizer = torch.optim.Adam(model.parameters(), lr=args.lr, weight_decay=args.weight_decay)
+    train_ids, val_ids, _ = split_ids(args)
+    packed = solver.PackedWeights()
+    history = []
+    for epoch in range(args.num_epoch):
+        model.train()
+        t0 = time.time()
+        loss = float("nan")
+        for bi in range(int(len(train_ids) / args.batch_size)):
+            ids = train_ids[bi * args.batch_size:(bi + 1) * args.batch_size]
+            first, count = parallel.shard(len(ids), world, rank)
+            d = _instances(args, ids[first:first + count], device)
+            if args.scaling:
+                Qs, ps, As, zls, zus, _, _, _ = ops.ruiz_scale(d["Q"], d["p"], d["A0"], d["zl"], d["zu"], args.scaling_ites)
+                d = dict(Q=Qs, p=ps, A0=As, zl=zls, zu=zus)
+            loss = train.tbptt_batch(model, d, mi, me, args.outer_T, args.truncated_length, args.sigma, optimizer,
+                                     micro_batch=args.micro_batch or None, global_batch=len(ids), dist=dist)
+        train_time = time.time() - t0
+        # validation: full unroll under no_grad (main.py:382-510), metrics on unscaled x
+        model.eval()
+        t0 = time.time()
+        with torch.no_grad():
+            v = _instances(args, val_ids, device)
+            out = solver.solve(model, v["Q"], v["p"], v["A0"], v["zl"], v["zu"], mi, me, args.outer_T, args.sigma,
+                               scaling=args.scaling, scaling_iters=args.scaling_ites, packed=packed)
+            x = out["x"].reshape(len(val_ids), -1).contiguous()
+            val_obj = float(out["obj"].mean())
+            vios = []
+            if mi:
+                vios.append(float(ops.bmv(v["G"].contiguous(), x, v["c"].reshape(len(val_ids), -1).contiguous(),
+                                          ops.BMV_POS_EXCESS).max(1).values.mean()))
+            if me:
+                vios.append(float(ops.bmv(v["A"].contiguous(), x, v["b"].reshape(len(val_ids), -1).contiguous(),
+                                          ops.BMV_ABS_GAP).max(1).values.mean()))
+        val_time = time.time() - t0
+        stop = False
+        if rank == 0:
+            stop = stopper.step(val_obj, model, args.early_stop_mode or "min", args.eq_tol, *vios)
+            print("Epoch : {} | Train_Loss : {:.4f} | Val_Obj : {:.3f} | Train_Time : {:.3f} | Val_Time : {:.3f} |".format(
+                epoch, loss, val_obj, train_time, val_time), flush=True)
+        if dist is not None:
+            flag = torch.tensor([1 if stop else 0], device=device)
+            dist.broadcast(flag, 0)
+            stop = bool(flag.item())
+        history.append((loss, val_obj))
+        if stop:
+            break
+    if dist is not None:
+        dist.destroy_process_group()
+    return history
+
+
 def main(argv=None):
     args = parse_args(argv)
     if args.test:
         return run_test(args)
-    raise SystemExit("training mode needs the backward kernels, which are not built yet (DESIGN.md §7)")
+    return run_train(args)
 
 
 if __name__ == "__main__":

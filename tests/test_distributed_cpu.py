@@ -73,3 +73,44 @@ def test_cli_parses_reference_command_line():
     assert (a.prob_type, a.outer_T, a.hidden_dim, a.test_outer_T) == ("QP", 100, 800, 100)
     assert a.scaling and a.test and a.save_sol
     assert a.sigma == pytest.approx(6e-6) and a.num_var == 5000 and a.weight_decay == 0.0
+
+
+def _ddp_worker(rank, world, port, q):
+    """Data-parallel training math on CPU tensors (gloo): each rank takes its shard of a batch,
+    scales its mean loss by shard/global size and the gradients are all-reduced; the result must
+    equal the single-process gradient of the full-batch mean."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    torch.set_num_threads(1)
+    from iadmm import train
+    dist = parallel.init("gloo")
+    torch.manual_seed(0)
+    model = torch.nn.Linear(5, 3)
+    X = torch.randn(7, 5)
+    first, count = parallel.shard(7, world, rank)
+    loss = model(X[first:first + count]).pow(2).sum(1).mean()
+    (count / 7 * loss).backward()
+    train.allreduce_grads(list(model.parameters()), dist, bucket_bytes=64)  # forces several buckets
+    if rank == 0:
+        q.put([p.grad.clone() for p in model.parameters()])
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_ddp_gradient_allreduce_equals_full_batch():
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_ddp_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    grads = q.get(timeout=240)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    torch.manual_seed(0)
+    model = torch.nn.Linear(5, 3)
+    X = torch.randn(7, 5)
+    model(X).pow(2).sum(1).mean().backward()
+    for g, p in zip(grads, model.parameters()):
+        assert torch.allclose(g, p.grad, atol=1e-6)

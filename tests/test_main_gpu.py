@@ -28,3 +28,21 @@ def test_main_test_mode(tmp_path, capsys):
     mat = sio.loadmat(os.path.join(tmp_path, "lstm", "QP_60_10_20_8_40_results.mat"))
     assert mat["primal_res"].shape == (2, 8)
     assert np.isfinite(mat["dual_res"]).all()
+
+
+def test_main_train_mode_improves_loss(tmp_path):
+    """main.py training mode (synthetic QPs): the TBPTT loss goes down over a few epochs and the
+    EarlyStopping checkpoint is written in the reference's .pth format."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import main
+    argv = ["--prob_type", "QP", "--num_var", "40", "--num_ineq", "16", "--num_eq", "8", "--outer_T", "10",
+            "--truncated_length", "5", "--hidden_dim", "32", "--sigma", "6e-6", "--scaling", "--lr", "0.002",
+            "--batch_size", "4", "--data_size", "40", "--val_frac", "0.1", "--test_frac", "0.1",
+            "--num_epoch", "4", "--eq_tol", "1e9", "--ineq_tol", "1e9", "--early_stop_mode", "min",
+            "--save_dir", str(tmp_path), "--synthetic", "--micro_batch", "2", "--patience", "10"]
+    hist = main.main(argv)
+    assert len(hist) == 4
+    assert hist[-1][0] < hist[0][0]
+    sd = torch.load(os.path.join(tmp_path, "lstm", "params", "QP_40_16_8_10_32.pth"), weights_only=True)
+    assert set(sd) >= {"W_i", "U_u", "W_h", "b_h", "rho", "alpha"}
