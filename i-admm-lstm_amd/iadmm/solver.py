@@ -204,6 +204,13 @@ def _unit_scal(like):
 STAGE2_ALPHA = 1.6  # models/lu.py:24
 
 
+def rho_rows_of(scal, B, m, num_ineq):
+    """Per-row rho [B,m] of a two-class schedule (models/lstm.py:61-62)."""
+    idx = torch.arange(m, device=scal.device)
+    row = torch.where(idx < num_ineq, scal[ops.S_RHO_IN], scal[ops.S_RHO_EQ])
+    return row.unsqueeze(0).expand(B, m).contiguous()
+
+
 def fixed_alpha_scal(alpha, device):
     """Iteration scalars carrying only a fixed relaxation (Stage II): alpha, fl32(1 - alpha)."""
     a = torch.tensor(alpha, dtype=torch.float32)
@@ -213,12 +220,12 @@ def fixed_alpha_scal(alpha, device):
     return s.to(device)
 
 
-def stage2(Q, p, A0, zl, zu, rho_rows, x, y, z, sigma, iters, alpha=STAGE2_ALPHA, timer=None):
+def stage2(Q, p, A0, zl, zu, rho_rows, x, y, z, sigma, iters, alpha=STAGE2_ALPHA, timer=None, iter_hook=None):
     """Stage II feasibility restoration (models/lu.py:13-47, driver main.py:1035-1066):
     factor K once (rho of the last Stage-I iteration), then ``iters`` exact ADMM steps with
     alpha-relaxation on x and z.  Works on the unscaled data like the reference.
     Q[B,n,n], p[B,n], A0[B,m,n], zl/zu/rho_rows[B,m], x[B,n], y/z[B,m].  Returns the iterates and
-    the factors (LU, piv)."""
+    the factors (LU, piv).  ``iter_hook(t, x, y, z)`` runs after every iteration (metrics)."""
     timer = timer or Timer(False)
     B, n = x.shape
     m = y.shape[1]
@@ -234,5 +241,7 @@ def stage2(Q, p, A0, zl, zu, rho_rows, x, y, z, sigma, iters, alpha=STAGE2_ALPHA
         xs = ops.lu_solve(LU, piv, b)
         xv, x, y, z = ops.admm_update(n, m, 0, None, None, xs, x, y, z, zl, zu, scal, relax_z=True,
                                       rho_rows=rho_rows)
+        if iter_hook is not None:
+            iter_hook(_, x, y, z)
     timer.stop(tok)
     return dict(x=x, y=y, z=z, xv=xv, LU=LU, piv=piv, info=info)

@@ -154,6 +154,30 @@ def run_test(args):
             total_time += sum(v for k, v in spans.items() if not k.startswith("k:")) / 1e3
             h = {k: out["hist_" + k].mean(1).cpu().numpy() for k in ("obj", "ls_res", "primal", "dual")}
             h["viol"] = viol.mean(2).cpu().numpy()
+            if args.feas_rest:  # Stage II on the unscaled data with the last rho (main.py:1035-1066)
+                F = args.feas_rest_num
+                fobj = torch.zeros(F, tb, device=device)
+                fvio = torch.zeros(4, F, tb, device=device)
+
+                def fhook(t, x, y, z):
+                    fobj[t] = ops.metrics(d["Q"], d["p"].reshape(tb, -1), d["A0"], x, y, z)[0]
+                    if mi:
+                        iv = ops.bmv(G, x, c, ops.BMV_POS_EXCESS)
+                        fvio[0, t], fvio[1, t] = iv.max(1).values, iv.mean(1)
+                    if me:
+                        ev = ops.bmv(A, x, b, ops.BMV_ABS_GAP)
+                        fvio[2, t], fvio[3, t] = ev.max(1).values, ev.mean(1)
+
+                ftimer = solver.Timer(True)
+                rho_rows = solver.rho_rows_of(out["scal"], tb, mi + me, mi)
+                s2 = solver.stage2(d["Q"], d["p"].reshape(tb, -1).contiguous(), d["A0"], d["zl"].reshape(tb, -1).contiguous(),
+                                   d["zu"].reshape(tb, -1).contiguous(), rho_rows, out["x"].reshape(tb, -1).contiguous(),
+                                   out["y"].reshape(tb, -1).contiguous(), out["z"].reshape(tb, -1).contiguous(),
+                                   args.sigma, F, timer=ftimer, iter_hook=fhook)
+                total_time += sum(ftimer.totals_ms().values()) / 1e3
+                h["fr_obj"] = fobj.mean(1).cpu().numpy()
+                h["fr_viol"] = fvio.mean(2).cpu().numpy()
+                out["x"] = s2["x"].unsqueeze(-1)
             reports.append(h)
             last = out
     mean = lambda k: np.mean([r[k] for r in reports], axis=0)  # noqa: E731
@@ -165,8 +189,16 @@ def run_test(args):
             print("Test_Max_Ineq : {:.3f} | Test_Mean_Ineq : {:.3f} |".format(vi[0, t], vi[1, t]))
         if me:
             print("Test_Max_Eq : {:.3f} | Test_Mean_Eq : {:.3f} |".format(vi[2, t], vi[3, t]))
-    if args.feas_rest:
-        raise SystemExit("--feas_rest needs the Stage II LU kernels (not built yet, DESIGN.md §7)")
+    if args.feas_rest:  # main.py:1140-1161
+        print("-----Starting Sage II-----")
+        fr = np.mean([r["fr_obj"] for r in reports], axis=0)
+        fv = np.mean([r["fr_viol"] for r in reports], axis=0)
+        for t in range(args.feas_rest_num):
+            print("Epoch : {} | Test_Obj : {:.3f}".format(t, fr[t]))
+            if mi:
+                print("Test_Max_Ineq : {:.3f} | Test_Mean_Ineq : {:.3f} |".format(fv[0, t], fv[1, t]))
+            if me:
+                print("Test_Max_Eq : {:.3f} | Test_Mean_Eq : {:.3f} |".format(fv[2, t], fv[3, t]))
     print("Parallel Time : {}".format(total_time / (nb * tb)))
     if args.save_sol:  # main.py:1172-1178, 1248-1268
         import scipy.io as sio

@@ -18,11 +18,13 @@ def test_main_test_mode(tmp_path, capsys):
     argv = ["--config", cfg, "--prob_type", "QP", "--num_var", "60", "--num_ineq", "20", "--num_eq", "10",
             "--outer_T", "8", "--hidden_dim", "40", "--scaling", "--test", "--test_outer_T", "8",
             "--test_batch_size", "4", "--data_size", "100", "--test_frac", "0.1", "--val_frac", "0.1",
-            "--save_sol", "--save_dir", str(tmp_path), "--synthetic", "--random_init"]
+            "--save_sol", "--save_dir", str(tmp_path), "--synthetic", "--random_init", "--feas_rest",
+            "--feas_rest_num", "3"]
     reports, total = main.main(argv)
     out = capsys.readouterr().out
     assert out.count("Primal_Residuals") == 8 and "Parallel Time" in out
     assert "Test_Max_Ineq" in out and "Test_Max_Eq" in out
+    assert "Starting Sage II" in out and out.count("Test_Obj") == 8 + 3
     assert len(reports) == 2 and total > 0
     import scipy.io as sio
     mat = sio.loadmat(os.path.join(tmp_path, "lstm", "QP_60_10_20_8_40_results.mat"))
