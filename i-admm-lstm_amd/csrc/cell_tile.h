@@ -13,6 +13,13 @@ constexpr int kBK = 32;          // K chunk
 constexpr int kLD = kBK + 4;     // padded LDS row (floats)
 constexpr int kWxF = 16;         // packed per-unit fields: Wi0 Wi1 bi Wf0 Wf1 bf Wo0 Wo1 bo Wu0 Wu1 bu Wh
 
+struct CellArgsT {
+  int64_t M;
+  int h, njt, nkc32;
+  const float *H, *C, *xv, *g, *Upk, *Wx;
+  float *Hn, *Cn, *part;
+};
+
 // XCD-aware bijective remap: blocks b, b+8, ... share an XCD; give each XCD a contiguous run of
 // logical tiles with the hidden tile fastest, so an H panel is reused from that XCD's L2.
 IADMM_DEV void cell_tile_of_block(int njt, int& jt, int& rt) {

@@ -57,6 +57,16 @@ inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 
 
 }  // namespace iadmm
 
+// Dynamic LDS above 64 KiB (gfx950 has 160 KiB per CU) must be opted into per kernel.
+#define IADMM_ALLOW_LDS(kernel, bytes)                                                        \
+  do {                                                                                         \
+    if ((bytes) > 65536) {                                                                     \
+      hipError_t e_ = hipFuncSetAttribute((const void*)(kernel),                               \
+                                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)(bytes)); \
+      if (e_ != hipSuccess) return static_cast<int>(e_);                                       \
+    }                                                                                          \
+  } while (0)
+
 #define IADMM_CHECK_LAUNCH()                          \
   do {                                                \
     hipError_t e_ = hipGetLastError();                \

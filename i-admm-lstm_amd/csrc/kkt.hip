@@ -253,7 +253,7 @@ int launch_kkt(int64_t B, int64_t n, int64_t m, KktArgs a, hipStream_t s) {
   const bool vec = (n % 4 == 0) && aligned16(a.Q) && (m == 0 || aligned16(a.A0));
   const size_t lds = (3 * n + 2 * m) * sizeof(float);
   IADMM_DISPATCH_NG(ng, vec, {
-    hipLaunchKernelGGL((kkt_kernel<NG_, V_, PASS2>), dim3((unsigned)B), dim3(kKktThreads), lds, s, a);
+    IADMM_ALLOW_LDS((kkt_kernel<NG_, V_, PASS2>), lds); hipLaunchKernelGGL((kkt_kernel<NG_, V_, PASS2>), dim3((unsigned)B), dim3(kKktThreads), lds, s, a);
   });
   IADMM_CHECK_LAUNCH();
   return 0;
@@ -296,7 +296,7 @@ extern "C" int iadmm_metrics(int64_t B, int64_t n, int64_t m, const float* Q, co
   const bool vec = (n % 4 == 0) && aligned16(Q) && (m == 0 || aligned16(A0));
   const size_t lds = (3 * n + 2 * m) * sizeof(float);
   IADMM_DISPATCH_NG(ng, vec, {
-    hipLaunchKernelGGL((metrics_kernel<NG_, V_>), dim3((unsigned)B), dim3(kKktThreads), lds,
+    IADMM_ALLOW_LDS((metrics_kernel<NG_, V_>), lds); hipLaunchKernelGGL((metrics_kernel<NG_, V_>), dim3((unsigned)B), dim3(kKktThreads), lds,
                        (hipStream_t)stream, a);
   });
   IADMM_CHECK_LAUNCH();
@@ -325,7 +325,7 @@ extern "C" int iadmm_bmv(int64_t B, int64_t R, int64_t C, const float* Mx, const
   const bool vec = (C % 4 == 0) && aligned16(Mx);
   const size_t lds = (R + C) * sizeof(float);
   IADMM_DISPATCH_NG(ng, vec, {
-    hipLaunchKernelGGL((bmv_kernel<NG_, V_>), dim3((unsigned)B), dim3(kKktThreads), lds,
+    IADMM_ALLOW_LDS((bmv_kernel<NG_, V_>), lds); hipLaunchKernelGGL((bmv_kernel<NG_, V_>), dim3((unsigned)B), dim3(kKktThreads), lds,
                        (hipStream_t)stream, (int)R, (int)C, Mx, x, rhs, mode, out);
   });
   IADMM_CHECK_LAUNCH();
@@ -345,9 +345,9 @@ extern "C" int iadmm_kkt_matvec(int64_t B, int64_t n, int64_t m, int64_t num_ine
   const size_t lds = (3 * n + 2 * m) * sizeof(float);
   hipStream_t s = (hipStream_t)stream;
   if (transpose) {
-    IADMM_DISPATCH_NG(ng, vec, { hipLaunchKernelGGL((kkt_matvec_kernel<NG_, V_, true>), dim3((unsigned)B), dim3(kKktThreads), lds, s, a, rho_rows, out); });
+    IADMM_DISPATCH_NG(ng, vec, { IADMM_ALLOW_LDS((kkt_matvec_kernel<NG_, V_, true>), lds); hipLaunchKernelGGL((kkt_matvec_kernel<NG_, V_, true>), dim3((unsigned)B), dim3(kKktThreads), lds, s, a, rho_rows, out); });
   } else {
-    IADMM_DISPATCH_NG(ng, vec, { hipLaunchKernelGGL((kkt_matvec_kernel<NG_, V_, false>), dim3((unsigned)B), dim3(kKktThreads), lds, s, a, rho_rows, out); });
+    IADMM_DISPATCH_NG(ng, vec, { IADMM_ALLOW_LDS((kkt_matvec_kernel<NG_, V_, false>), lds); hipLaunchKernelGGL((kkt_matvec_kernel<NG_, V_, false>), dim3((unsigned)B), dim3(kKktThreads), lds, s, a, rho_rows, out); });
   }
   IADMM_CHECK_LAUNCH();
   return 0;

@@ -262,10 +262,7 @@ extern "C" int iadmm_lu_factor(int64_t B, int64_t N, float* A, int* piv, int* in
   const size_t lds = ((size_t)N * kPS + 16) * sizeof(float);
   if (lds > 160 * 1024 || B > 0x7fffffff) return IADMM_E_SIZE;
   hipStream_t s = (hipStream_t)stream;
-  if (lds > 64 * 1024) {
-    hipError_t e = hipFuncSetAttribute((const void*)lu_panel_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    if (e != hipSuccess) return (int)e;
-  }
+  IADMM_ALLOW_LDS(lu_panel_kernel, lds);
   hipError_t e = hipMemsetAsync(info, 0, B * sizeof(int), s);
   if (e != hipSuccess) return (int)e;
   const bool vec = (N % 4 == 0) && aligned16(A);

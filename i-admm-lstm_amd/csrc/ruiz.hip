@@ -239,7 +239,7 @@ extern "C" int iadmm_ruiz_scale(int64_t B, int64_t n, int64_t m, int64_t iters, 
                    (m == 0 || (aligned16(A0) && aligned16(A0_out)));
   const size_t lds = (3 * n + 2 * m + 8) * sizeof(float);
   IADMM_DISPATCH_NG(ng, vec, {
-    hipLaunchKernelGGL((ruiz_kernel<NG_, V_>), dim3((unsigned)B), dim3(kRuizThreads), lds,
+    IADMM_ALLOW_LDS((ruiz_kernel<NG_, V_>), lds); hipLaunchKernelGGL((ruiz_kernel<NG_, V_>), dim3((unsigned)B), dim3(kRuizThreads), lds,
                        (hipStream_t)stream, a);
   });
   IADMM_CHECK_LAUNCH();

@@ -451,7 +451,7 @@ extern "C" int iadmm_kkt_bwd(int64_t B, int64_t n, int64_t m, int64_t num_ineq, 
   const bool vec = (n % 4 == 0) && aligned16(Q) && (m == 0 || aligned16(A0));
   const size_t lds = (3 * n + 2 * m) * sizeof(float);
   IADMM_DISPATCH_NG(ng, vec, {
-    hipLaunchKernelGGL((kkt_bwd_kernel<NG_, V_>), dim3((unsigned)B), dim3(256), lds, (hipStream_t)stream, a);
+    IADMM_ALLOW_LDS((kkt_bwd_kernel<NG_, V_>), lds); hipLaunchKernelGGL((kkt_bwd_kernel<NG_, V_>), dim3((unsigned)B), dim3(256), lds, (hipStream_t)stream, a);
   });
   IADMM_CHECK_LAUNCH();
   return 0;
@@ -477,7 +477,7 @@ extern "C" int iadmm_loss_grad(int64_t B, int64_t n, int64_t m, const float* Q, 
   const bool vec = (n % 4 == 0) && aligned16(Q) && (m == 0 || aligned16(A0));
   const size_t lds = (3 * n + 2 * m) * sizeof(float);
   IADMM_DISPATCH_NG(ng, vec, {
-    hipLaunchKernelGGL((loss_grad_kernel<NG_, V_>), dim3((unsigned)B), dim3(256), lds, (hipStream_t)stream, a);
+    IADMM_ALLOW_LDS((loss_grad_kernel<NG_, V_>), lds); hipLaunchKernelGGL((loss_grad_kernel<NG_, V_>), dim3((unsigned)B), dim3(256), lds, (hipStream_t)stream, a);
   });
   IADMM_CHECK_LAUNCH();
   return 0;

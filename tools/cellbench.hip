@@ -1,0 +1,140 @@
+// Variant microbenchmark of the fused LSTM-cell kernel at the bench shape (M = 1024*2000 rows,
+// h = 800): interleaved rounds of every variant in one process (cdna_hip_programming.md §5.4
+// rule 24), hipEvent timing, TFLOP/s on the algorithmic 8*M*h^2 + 18*M*h flops.
+// Build: hipcc -O3 -std=c++17 --offload-arch=gfx950 -ffp-contract=off tools/cellbench.hip -o /tmp/cellbench
+#include "../i-admm-lstm_amd/csrc/cell_kernel.h"
+
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+#include <string>
+#include <algorithm>
+
+using namespace iadmm;
+
+#define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP error %s at %d\n", hipGetErrorString(e), __LINE__); exit(1); } } while (0)
+
+__global__ void fill(float* p, int64_t n, uint32_t seed, float scale) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    uint32_t x = (uint32_t)i * 2654435761u ^ seed;
+    x ^= x >> 13; x *= 0x5bd1e995u; x ^= x >> 15;
+    p[i] = scale * ((x & 0xffffff) / 16777216.0f * 2.f - 1.f);
+  }
+}
+
+// Pure-MFMA ceiling at the cell kernel's register shape (8 accumulators, operands in registers,
+// same grid and occupancy): how many fp32 MFMA TFLOP/s this device sustains under load.
+typedef float floatx4 __attribute__((ext_vector_type(4)));
+template <int SHAPE>
+__global__ __launch_bounds__(256, 2) void mfma_ceiling(int iters, float* out, float seed) {
+  const int lane = threadIdx.x & 63;
+  float av = seed * (lane + 1), bv = seed * (lane + 3);
+  if constexpr (SHAPE == 32) {
+    floatx16 acc[8];
+    for (int i = 0; i < 8; ++i) for (int q = 0; q < 16; ++q) acc[i][q] = 0.f;
+    for (int it = 0; it < iters; ++it) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) acc[i] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv + i, acc[i], 0, 0, 0);
+    }
+    float s = 0.f;
+    for (int i = 0; i < 8; ++i) for (int q = 0; q < 16; ++q) s += acc[i][q];
+    out[blockIdx.x * 256 + threadIdx.x] = s;
+  } else {
+    floatx4 acc[32];
+    for (int i = 0; i < 32; ++i) for (int q = 0; q < 4; ++q) acc[i][q] = 0.f;
+    for (int it = 0; it < iters; ++it) {
+#pragma unroll
+      for (int i = 0; i < 32; ++i) acc[i] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv + i, acc[i], 0, 0, 0);
+    }
+    float s = 0.f;
+    for (int i = 0; i < 32; ++i) for (int q = 0; q < 4; ++q) s += acc[i][q];
+    out[blockIdx.x * 256 + threadIdx.x] = s;
+  }
+}
+
+struct Variant {
+  std::string name;
+  void (*launch)(CellArgsT, int64_t, hipStream_t);
+};
+
+template <int NW, int BK, bool DBUF, bool FAST, int EPI>
+void launch_v(CellArgsT a, int64_t M, hipStream_t s) {
+  const int64_t rows = 64 * NW;
+  const int64_t nrt = (M + rows - 1) / rows;
+  hipLaunchKernelGGL((cell_fwd_kernel<NW, BK, DBUF, FAST, EPI, true>), dim3((unsigned)(nrt * a.njt)), dim3(64 * NW), 0, s, a);
+}
+
+int main(int argc, char** argv) {
+  const int64_t B = argc > 1 ? atoll(argv[1]) : 1024;
+  const int64_t N = 2000, h = 800;
+  const int64_t M = B * N;
+  const int rounds = argc > 2 ? atoi(argv[2]) : 5;
+  const int njt = (h + 31) / 32, nkc32 = (h + 31) / 32;
+  float *H, *C, *xv, *g, *Upk, *Wx, *Hn, *Cn, *part;
+  CK(hipMalloc(&H, M * h * 4)); CK(hipMalloc(&C, M * h * 4)); CK(hipMalloc(&Hn, M * h * 4)); CK(hipMalloc(&Cn, M * h * 4));
+  CK(hipMalloc(&xv, M * 4)); CK(hipMalloc(&g, M * 4)); CK(hipMalloc(&part, (int64_t)njt * M * 4));
+  const int64_t nup = (int64_t)njt * nkc32 * 128 * 32, nwx = (int64_t)njt * 32 * 16;
+  CK(hipMalloc(&Upk, nup * 4)); CK(hipMalloc(&Wx, nwx * 4));
+  hipLaunchKernelGGL(fill, dim3(4096), dim3(256), 0, 0, H, M * h, 1u, 0.9f);
+  hipLaunchKernelGGL(fill, dim3(4096), dim3(256), 0, 0, C, M * h, 2u, 0.5f);
+  hipLaunchKernelGGL(fill, dim3(4096), dim3(256), 0, 0, xv, M, 3u, 1.0f);
+  hipLaunchKernelGGL(fill, dim3(4096), dim3(256), 0, 0, g, M, 4u, 1.0f);
+  hipLaunchKernelGGL(fill, dim3(4096), dim3(256), 0, 0, Upk, nup, 5u, 0.02f);
+  hipLaunchKernelGGL(fill, dim3(256), dim3(256), 0, 0, Wx, nwx, 6u, 0.02f);
+  CK(hipDeviceSynchronize());
+  CellArgsT a{M, (int)h, njt, nkc32, H, C, xv, g, Upk, Wx, Hn, Cn, part};
+  std::vector<Variant> vs = {
+      {"NW4 BK32 single  precise", launch_v<4, 32, false, false, 0>},
+      {"NW4 BK32 single  fast   ", launch_v<4, 32, false, true, 0>},
+      {"NW4 BK32 single  noepi  ", launch_v<4, 32, false, false, 1>},
+      {"NW4 BK16 dbuf    precise", launch_v<4, 16, true, false, 0>},
+      {"NW4 BK16 dbuf    fast   ", launch_v<4, 16, true, true, 0>},
+      {"NW4 BK16 dbuf    noepi  ", launch_v<4, 16, true, false, 1>},
+      {"NW8 BK16 dbuf    precise", launch_v<8, 16, true, false, 0>},
+      {"NW8 BK16 dbuf    fast   ", launch_v<8, 16, true, true, 0>},
+      {"NW8 BK16 dbuf    noepi  ", launch_v<8, 16, true, false, 1>},
+      {"NW8 BK32 single  precise", launch_v<8, 32, false, false, 0>},
+  };
+  const double flop = (8.0 * h * h + 18.0 * h) * M;
+  hipStream_t s;
+  CK(hipStreamCreate(&s));
+  std::vector<std::vector<float>> t(vs.size());
+  for (auto& v : vs) { v.launch(a, M, s); }  // warm-up
+  CK(hipStreamSynchronize(s));
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
+  for (int r = 0; r < rounds; ++r) {
+    for (size_t i = 0; i < vs.size(); ++i) {
+      CK(hipEventRecord(e0, s));
+      vs[i].launch(a, M, s);
+      CK(hipEventRecord(e1, s));
+      CK(hipEventSynchronize(e1));
+      float ms;
+      CK(hipEventElapsedTime(&ms, e0, e1));
+      t[i].push_back(ms);
+    }
+  }
+  CK(hipGetLastError());
+  printf("M=%lld h=%lld rounds=%d\n", (long long)M, (long long)h, rounds);
+  {  // MFMA ceiling: 512 blocks x 4 waves, each wave 8 x 32x32x2 (or 32 x 16x16x4) per iteration
+    const int iters = 20000, blocks = 512;
+    for (int shape : {32, 16, 32, 16}) {
+      CK(hipEventRecord(e0, s));
+      if (shape == 32) hipLaunchKernelGGL(mfma_ceiling<32>, dim3(blocks), dim3(256), 0, s, iters, part, 1e-3f);
+      else hipLaunchKernelGGL(mfma_ceiling<16>, dim3(blocks), dim3(256), 0, s, iters, part, 1e-3f);
+      CK(hipEventRecord(e1, s));
+      CK(hipEventSynchronize(e1));
+      float ms;
+      CK(hipEventElapsedTime(&ms, e0, e1));
+      const double f = (double)blocks * 4 * iters * 8 * 4096.0;  // both shapes: 32768 flop per wave-iteration
+      printf("MFMA ceiling %dx%d f32: %8.3f ms  %7.1f TFLOP/s\n", shape, shape, ms, f / (ms * 1e-3) / 1e12);
+    }
+  }
+  for (size_t i = 0; i < vs.size(); ++i) {
+    auto v = t[i];
+    std::sort(v.begin(), v.end());
+    const float med = v[v.size() / 2];
+    printf("%s  median %8.3f ms  min %8.3f ms  %7.1f TFLOP/s (median)\n", vs[i].name.c_str(), med, v[0], flop / (med * 1e-3) / 1e12);
+  }
+  return 0;
+}
