@@ -25,11 +25,11 @@ def test_config4_shape_vs_oracle():
     n, mi, me, h, T = 5000, 2500, 2500, 2048, 2
     d = data.make_qp_batch(n, mi, me, 1, first_index=0, device="cuda")
     params = data.init_lstm_params(h, 200, device="cuda")
+    cpu = {k: v.cpu() for k, v in d.items()}  # before the in-place scaling below
     with torch.no_grad():
         out = solver.solve(params, d["Q"], d["p"], d["A0"], d["zl"], d["zu"], mi, me, T, 6e-6, keep_unscaled=False)
     torch.cuda.synchronize()
     torch.set_num_threads(max(1, min(16, torch.get_num_threads())))
-    cpu = {k: v.cpu() for k, v in d.items()}
     with torch.no_grad():
         ref = orc.solve({k: v.cpu() for k, v in params.items()}, cpu["Q"], cpu["p"], cpu["A0"], cpu["zl"],
                         cpu["zu"], mi, me, T, 6e-6, h)
