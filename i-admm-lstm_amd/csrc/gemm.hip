@@ -19,7 +19,7 @@ typedef float floatx16 __attribute__((ext_vector_type(16)));
 constexpr int kGBK = 32;
 constexpr int kGLD = kGBK + 4;
 
-template <bool ACC>
+template <bool ACC, bool VEC>
 __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(int64_t M, int Ni, int K, const float* X,
                                                          const float* W, float* out) {
   __shared__ __attribute__((aligned(16))) float sA[128 * kGLD];
@@ -38,18 +38,45 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(int64_t M, int Ni, int 
 #pragma unroll
       for (int q = 0; q < 16; ++q) acc[g][r][q] = 0.f;
   const int nkc = (K + kGBK - 1) / kGBK;
+  float4 ra[4], rb[8];
+  auto ld4 = [&](const float* base, int64_t row, int64_t nrow, int k) -> float4 {
+    if constexpr (VEC) {
+      return (row < nrow && k < K) ? *reinterpret_cast<const float4*>(base + row * K + k)
+                                   : make_float4(0.f, 0.f, 0.f, 0.f);
+    } else {
+      float4 t;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) set4(t, e, (row < nrow && k + e < K) ? base[row * K + k + e] : 0.f);
+      return t;
+    }
+  };
+  auto gload = [&](int kc) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int idx = tid + 256 * q, row = idx >> 3, c4 = idx & 7;
+      ra[q] = ld4(W, i0 + row, Ni, kc * kGBK + c4 * 4);
+    }
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int idx = tid + 256 * q, row = idx >> 3, c4 = idx & 7;
+      rb[q] = ld4(X, r0 + row, M, kc * kGBK + c4 * 4);
+    }
+  };
+  gload(0);
   for (int kc = 0; kc < nkc; ++kc) {
     __syncthreads();
-    for (int idx = tid; idx < 128 * kGBK; idx += 256) {
-      const int row = idx / kGBK, kk = idx % kGBK, k = kc * kGBK + kk, i = i0 + row;
-      sA[row * kGLD + kk] = (i < Ni && k < K) ? W[(int64_t)i * K + k] : 0.f;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int idx = tid + 256 * q, row = idx >> 3, c4 = idx & 7;
+      *reinterpret_cast<float4*>(&sA[row * kGLD + c4 * 4]) = ra[q];
     }
-    for (int idx = tid; idx < 256 * kGBK; idx += 256) {
-      const int row = idx / kGBK, kk = idx % kGBK, k = kc * kGBK + kk;
-      const int64_t r = r0 + row;
-      sB[row * kGLD + kk] = (r < M && k < K) ? X[r * K + k] : 0.f;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int idx = tid + 256 * q, row = idx >> 3, c4 = idx & 7;
+      *reinterpret_cast<float4*>(&sB[row * kGLD + c4 * 4]) = rb[q];
     }
     __syncthreads();
+    if (kc + 1 < nkc) gload(kc + 1);
 #pragma unroll
     for (int G = 0; G < kGBK / 8; ++G) {
       float4 af[4], bf[2];
@@ -68,6 +95,7 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(int64_t M, int Ni, int 
             acc[g][r] = __builtin_amdgcn_mfma_f32_32x32x2f32(get4(af[g], s), get4(bf[r], s), acc[g][r], 0, 0, 0);
     }
   }
+  // epilogue: accumulator q of lane (jl,hf) = out[row jl][i0 + g*32 + (q&3) + 8(q>>2) + 4hf]
 #pragma unroll
   for (int r = 0; r < 2; ++r) {
     const int64_t R = r0 + wave * 64 + r * 32 + jl;
@@ -75,11 +103,20 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(int64_t M, int Ni, int 
 #pragma unroll
     for (int g = 0; g < 4; ++g)
 #pragma unroll
-      for (int q = 0; q < 16; ++q) {
-        const int i = i0 + g * 32 + (q & 3) + 8 * (q >> 2) + 4 * hf;
-        if (i < Ni) {
-          float* o = out + R * Ni + i;
-          *o = ACC ? *o + acc[g][r][q] : acc[g][r][q];
+      for (int qq = 0; qq < 4; ++qq) {
+        const int ib = i0 + g * 32 + 8 * qq + 4 * hf;
+        float* o = out + R * Ni + ib;
+        if (VEC && ib + 3 < Ni) {
+          float4 v = make_float4(acc[g][r][4 * qq], acc[g][r][4 * qq + 1], acc[g][r][4 * qq + 2], acc[g][r][4 * qq + 3]);
+          if (ACC) {
+            const float4 p = *reinterpret_cast<const float4*>(o);
+            v.x += p.x; v.y += p.y; v.z += p.z; v.w += p.w;
+          }
+          *reinterpret_cast<float4*>(o) = v;
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            if (ib + e < Ni) o[e] = ACC ? o[e] + acc[g][r][4 * qq + e] : acc[g][r][4 * qq + e];
         }
       }
   }
@@ -88,8 +125,8 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(int64_t M, int Ni, int 
 // Partial slab of X[rows, Ni]^T . Y[rows, No] for the row slice of blockIdx.z.
 __global__ __launch_bounds__(256, 2) void gemm_tn_kernel(int64_t M, int Ni, int No, int64_t rows_per_split,
                                                          const float* X, const float* Y, float* slab) {
-  __shared__ float sX[kGBK][128 + 4];
-  __shared__ float sY[kGBK][128 + 4];
+  __shared__ __attribute__((aligned(16))) float sX[kGBK][128 + 4];
+  __shared__ __attribute__((aligned(16))) float sY[kGBK][128 + 4];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, jl = lane & 31, hf = lane >> 5;
   const int i0 = blockIdx.x * 128, o0 = blockIdx.y * 128;
   const int64_t rbeg = (int64_t)blockIdx.z * rows_per_split;
@@ -102,14 +139,21 @@ __global__ __launch_bounds__(256, 2) void gemm_tn_kernel(int64_t M, int Ni, int 
     for (int c = 0; c < 2; ++c)
 #pragma unroll
       for (int q = 0; q < 16; ++q) acc[a][c][q] = 0.f;
+  const bool vx = (Ni % 4 == 0) && aligned16(X), vy = (No % 4 == 0) && aligned16(Y);
   for (int64_t rc = rbeg; rc < rend; rc += kGBK) {
     __syncthreads();
-    for (int idx = tid; idx < kGBK * 128; idx += 256) {
-      const int rr = idx / 128, cc = idx % 128;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {  // 32 rows x 32 float4 per operand, 4 per thread
+      const int idx = tid + 256 * q, rr = idx >> 5, c4 = (idx & 31) * 4;
       const int64_t r = rc + rr;
       const bool ok = r < rend;
-      sX[rr][cc] = (ok && i0 + cc < Ni) ? X[r * Ni + i0 + cc] : 0.f;
-      sY[rr][cc] = (ok && o0 + cc < No) ? Y[r * No + o0 + cc] : 0.f;
+      float4 tx, ty;
+      if (vx && i0 + c4 + 3 < Ni) tx = ok ? *reinterpret_cast<const float4*>(X + r * Ni + i0 + c4) : make_float4(0.f, 0.f, 0.f, 0.f);
+      else for (int e = 0; e < 4; ++e) set4(tx, e, (ok && i0 + c4 + e < Ni) ? X[r * Ni + i0 + c4 + e] : 0.f);
+      if (vy && o0 + c4 + 3 < No) ty = ok ? *reinterpret_cast<const float4*>(Y + r * No + o0 + c4) : make_float4(0.f, 0.f, 0.f, 0.f);
+      else for (int e = 0; e < 4; ++e) set4(ty, e, (ok && o0 + c4 + e < No) ? Y[r * No + o0 + c4 + e] : 0.f);
+      *reinterpret_cast<float4*>(&sX[rr][c4]) = tx;
+      *reinterpret_cast<float4*>(&sY[rr][c4]) = ty;
     }
     __syncthreads();
 #pragma unroll 4
@@ -159,10 +203,15 @@ extern "C" int iadmm_gemm_nt(int64_t M, int64_t Ni, int64_t K, const float* X, c
   const int64_t nit = (Ni + 127) / 128, nrt = (M + 255) / 256;
   if (nit * nrt > 0x7fffffffLL || Ni > (1 << 20) || K > (1 << 20)) return IADMM_E_SIZE;
   const dim3 grid((unsigned)(nit * nrt));
-  if (accumulate)
-    hipLaunchKernelGGL(gemm_nt_kernel<true>, grid, dim3(256), 0, (hipStream_t)stream, M, (int)Ni, (int)K, X, W, out);
-  else
-    hipLaunchKernelGGL(gemm_nt_kernel<false>, grid, dim3(256), 0, (hipStream_t)stream, M, (int)Ni, (int)K, X, W, out);
+  const bool vec = (K % 4 == 0) && (Ni % 4 == 0) && aligned16(X) && aligned16(W) && aligned16(out);
+  hipStream_t s = (hipStream_t)stream;
+  if (accumulate) {
+    if (vec) hipLaunchKernelGGL((gemm_nt_kernel<true, true>), grid, dim3(256), 0, s, M, (int)Ni, (int)K, X, W, out);
+    else hipLaunchKernelGGL((gemm_nt_kernel<true, false>), grid, dim3(256), 0, s, M, (int)Ni, (int)K, X, W, out);
+  } else {
+    if (vec) hipLaunchKernelGGL((gemm_nt_kernel<false, true>), grid, dim3(256), 0, s, M, (int)Ni, (int)K, X, W, out);
+    else hipLaunchKernelGGL((gemm_nt_kernel<false, false>), grid, dim3(256), 0, s, M, (int)Ni, (int)K, X, W, out);
+  }
   IADMM_CHECK_LAUNCH();
   return 0;
 }

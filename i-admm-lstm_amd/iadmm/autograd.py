@@ -95,7 +95,7 @@ class LossFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, y, z, data):
         Q, pv, A0 = data
-        pr, du, _, _, _ = ops.loss_grad(Q, pv, A0, x, y, z, want_grad=False)
+        _, pr, du = ops.metrics(Q, pv, A0, x, y, z)   # one sweep; the gradient sweep runs in backward
         ctx.save_for_backward(x, y, z)
         ctx.data = data
         return pr, du

@@ -75,3 +75,27 @@ def test_loss_grad_matches_autograd():
     ((a + 2 * b_) * w.float().cuda()).sum().backward()
     for mine, ref in ((xg, x), (yg, y), (zg, z)):
         assert rel_l2(mine.grad, ref.grad) < 1e-5
+
+
+@pytest.mark.parametrize("M,Ni,K", [(300, 40, 160), (1000, 130, 96), (257, 3, 50), (64, 800, 3200)])
+def test_gemm_nt_matches_fp64(M, Ni, K):
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from iadmm import ops
+    g = torch.Generator().manual_seed(M + Ni)
+    X, W = torch.randn(M, K, generator=g), torch.randn(Ni, K, generator=g)
+    out = ops.gemm_nt(X.cuda(), W.cuda())
+    assert rel_l2(out, X.double() @ W.double().T) < 1e-6
+    acc = ops.gemm_nt(X.cuda(), W.cuda(), out=out.clone(), accumulate=True)
+    assert rel_l2(acc, 2 * (X.double() @ W.double().T)) < 1e-6
+
+
+@pytest.mark.parametrize("M,Ni,No", [(300, 40, 160), (5000, 130, 96), (4099, 3, 50)])
+def test_gemm_tn_matches_fp64(M, Ni, No):
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from iadmm import ops
+    g = torch.Generator().manual_seed(M + No)
+    X, Y = torch.randn(M, Ni, generator=g), torch.randn(M, No, generator=g)
+    out = ops.gemm_tn(X.cuda(), Y.cuda(), rows_per_split=1024)
+    assert rel_l2(out, X.double().T @ Y.double()) < 1e-6
