@@ -85,9 +85,10 @@ def test_gemm_nt_matches_fp64(M, Ni, K):
     g = torch.Generator().manual_seed(M + Ni)
     X, W = torch.randn(M, K, generator=g), torch.randn(Ni, K, generator=g)
     out = ops.gemm_nt(X.cuda(), W.cuda())
-    assert rel_l2(out, X.double() @ W.double().T) < 1e-6
+    tol = 5e-8 * K ** 0.5  # fp32 accumulation over K random terms
+    assert rel_l2(out, X.double() @ W.double().T) < tol
     acc = ops.gemm_nt(X.cuda(), W.cuda(), out=out.clone(), accumulate=True)
-    assert rel_l2(acc, 2 * (X.double() @ W.double().T)) < 1e-6
+    assert rel_l2(acc, 2 * (X.double() @ W.double().T)) < tol
 
 
 @pytest.mark.parametrize("M,Ni,No", [(300, 40, 160), (5000, 130, 96), (4099, 3, 50)])
@@ -98,4 +99,4 @@ def test_gemm_tn_matches_fp64(M, Ni, No):
     g = torch.Generator().manual_seed(M + No)
     X, Y = torch.randn(M, Ni, generator=g), torch.randn(M, No, generator=g)
     out = ops.gemm_tn(X.cuda(), Y.cuda(), rows_per_split=1024)
-    assert rel_l2(out, X.double().T @ Y.double()) < 1e-6
+    assert rel_l2(out, X.double().T @ Y.double()) < 5e-8 * M ** 0.5
