@@ -9,6 +9,7 @@
 #include <vector>
 #include <string>
 #include <algorithm>
+#include <cmath>
 
 using namespace iadmm;
 
@@ -64,6 +65,12 @@ void launch_v(CellArgsT a, int64_t M, hipStream_t s) {
   hipLaunchKernelGGL((cell_fwd_kernel<NW, BK, DBUF, FAST, EPI, true>), dim3((unsigned)(nrt * a.njt)), dim3(64 * NW), 0, s, a);
 }
 
+template <bool FAST, int EPI>
+void launch_16(CellArgsT a, int64_t M, hipStream_t s) {
+  const int64_t nrt = (M + 255) / 256;
+  hipLaunchKernelGGL((cell_fwd16_kernel<FAST, EPI>), dim3((unsigned)(nrt * a.njt)), dim3(256), 0, s, a);
+}
+
 int main(int argc, char** argv) {
   const int64_t B = argc > 1 ? atoll(argv[1]) : 1024;
   const int64_t N = 2000, h = 800;
@@ -94,6 +101,9 @@ int main(int argc, char** argv) {
       {"NW8 BK16 dbuf    fast   ", launch_v<8, 16, true, true, 0>},
       {"NW8 BK16 dbuf    noepi  ", launch_v<8, 16, true, false, 1>},
       {"NW8 BK32 single  precise", launch_v<8, 32, false, false, 0>},
+      {"16x16x4 BK32     precise", launch_16<false, 0>},
+      {"16x16x4 BK32     fast   ", launch_16<true, 0>},
+      {"16x16x4 BK32     noepi  ", launch_16<false, 1>},
   };
   const double flop = (8.0 * h * h + 18.0 * h) * M;
   hipStream_t s;
@@ -115,6 +125,20 @@ int main(int argc, char** argv) {
     }
   }
   CK(hipGetLastError());
+  {  // cross-check: 32x32x2 and 16x16x4 variants produce the same H', C', part (fp32 rounding)
+    std::vector<float> h1(1 << 20), h2(1 << 20), p1(1 << 18), p2(1 << 18);
+    launch_v<4, 32, false, false, 0>(a, M, s);
+    CK(hipMemcpyAsync(h1.data(), Hn, h1.size() * 4, hipMemcpyDeviceToHost, s));
+    CK(hipMemcpyAsync(p1.data(), part, p1.size() * 4, hipMemcpyDeviceToHost, s));
+    launch_16<false, 0>(a, M, s);
+    CK(hipMemcpyAsync(h2.data(), Hn, h2.size() * 4, hipMemcpyDeviceToHost, s));
+    CK(hipMemcpyAsync(p2.data(), part, p2.size() * 4, hipMemcpyDeviceToHost, s));
+    CK(hipStreamSynchronize(s));
+    double dh = 0, nh = 0, dp = 0, np_ = 0;
+    for (size_t i = 0; i < h1.size(); ++i) { dh += (h1[i] - h2[i]) * (double)(h1[i] - h2[i]); nh += h1[i] * (double)h1[i]; }
+    for (size_t i = 0; i < p1.size(); ++i) { dp += (p1[i] - p2[i]) * (double)(p1[i] - p2[i]); np_ += p1[i] * (double)p1[i]; }
+    printf("cross-check 16x16 vs 32x32: rel-L2 H' %.3e  part %.3e\n", sqrt(dh / nh), sqrt(dp / np_));
+  }
   printf("M=%lld h=%lld rounds=%d\n", (long long)M, (long long)h, rounds);
   {  // MFMA ceiling: 512 blocks x 4 waves, each wave 8 x 32x32x2 (or 32 x 16x16x4) per iteration
     const int iters = 20000, blocks = 512;
