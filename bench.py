@@ -48,7 +48,10 @@ def parse():
     ap.add_argument("--cpu-sample", type=int, default=8, help="instances in the CPU baseline (0: skip)")
     ap.add_argument("--in-place-scaling", action="store_true",
                     help="scale Q/A0 in place (no unscaled copy; residuals via the scaling identity)")
-    return ap.parse_args()
+    a = ap.parse_args()
+    if a.in_place_scaling and a.warmup + a.steps == 1 and a.cpu_sample > 0:
+        ap.error("a single in-place step keeps no unscaled copy for the CPU baseline: add --cpu-sample 0")
+    return a
 
 
 def pmc_traffic(kernel_prefix, n, m, h, B):
@@ -68,6 +71,15 @@ def pmc_traffic(kernel_prefix, n, m, h, B):
             return None
         tot += mult * float(rows[0]["mean"]) * 1024.0
     return tot
+
+
+def baseline_config(args, world):
+    shape = (args.num_var, args.num_ineq, args.num_eq, args.hidden_dim, args.outer_T, args.batch)
+    if shape == (1000, 500, 500, 800, 100, 1024):
+        return "BASELINE config 2" if world == 1 else "BASELINE config 3"
+    if shape == (5000, 2500, 2500, 2048, 200, 512):
+        return "BASELINE config 4"
+    return "custom shape"
 
 
 def cpu_baseline(args, d, params):
@@ -103,11 +115,16 @@ def main():
     params = data.init_lstm_params(h, T, device="cuda")
     packed = solver.PackedWeights()
     keep = not args.in_place_scaling
-    if not keep:
-        master = {k: v.clone() for k, v in d.items()}  # restored before every step (untimed)
+    if not keep and args.warmup + args.steps > 1:
+        # restored before every step (untimed); on the host when a device copy would not fit
+        # (config 4: Q and A0 are 102 GB per GPU)
+        big = sum(v.numel() * 4 for v in d.values()) > 0.2 * torch.cuda.get_device_properties(local).total_memory
+        master = {k: v.to("cpu" if big else v.device, copy=True) for k, v in d.items()}
+    elif not keep:
+        master = None
 
     def step(timer):
-        if not keep:
+        if not keep and master is not None:
             for k in d:
                 d[k].copy_(master[k])
             torch.cuda.synchronize()
@@ -118,6 +135,7 @@ def main():
     for _ in range(args.warmup):
         step(None)
     torch.cuda.synchronize()
+    print(f"[bench] rank {rank} data + warmup ready", file=sys.stderr, flush=True)
 
     timer = solver.Timer(True)
     elapsed = 0.0
@@ -130,6 +148,7 @@ def main():
         out = step(timer)
         torch.cuda.synchronize()
         elapsed += time.perf_counter() - t0
+        print(f"[bench] rank {rank} step done, {time.perf_counter() - t0:.2f} s", file=sys.stderr, flush=True)
     elapsed = parallel.max_over_ranks(elapsed, dist, device="cuda")
     primal, dual = float(out["primal"].mean()), float(out["dual"].mean())
 
@@ -159,7 +178,7 @@ def main():
             "dtype": "f32",
             "data": "synthetic (generate_data.py:67-76 distribution, per-instance seeds; random-init weights)",
             "config": {"workload": f"QP n={n} ineq={mi} eq={me} K={T} hidden={h} --test --scaling, "
-                                   f"batch={B}/GPU (BASELINE config {'2' if world == 1 else '3'})",
+                                   f"batch={B}/GPU ({baseline_config(args, world)})",
                        "global_batch": world * B, "num_var": n, "num_ineq": mi, "num_eq": me,
                        "outer_T": T, "hidden_dim": h, "parallelism": f"instance-shard x{world}",
                        "in_place_scaling": not keep},

@@ -4,8 +4,9 @@ Same flag names and YAML config as the reference (main.py:22-62; ``-c/--config``
 unknown keys are ignored like ``parse_known_args``), plus ``--weight_decay`` which the reference
 reads but never registers (main.py:191).  Implemented modes:
 
-  --test   the test loop of main.py:549-1268 for prob_type QP: load instances
-           (./datasets/QP_{n}_{ineq}_{eq}/qp_{id}.gz, the reference's gz-pickled dicts, or
+  --test   the test loop of main.py:549-1268: load instances (./datasets/QP_{n}_{ineq}_{eq}/
+           qp_{id}.gz and the other prob_type layouts of iadmm/dataset.py, the reference's
+           gz-pickled dicts, or
            ``--synthetic`` instances from the generate_data.py:67-76 distribution), Ruiz-scale,
            ``test_outer_T`` Stage-I iterations, unscale, per-iteration report on unscaled data,
            "Parallel Time" and the optional ``--save_sol`` .mat file.  All compute runs in
@@ -18,9 +19,7 @@ reads but never registers (main.py:191).  Implemented modes:
            every batch and the gradients are all-reduced over RCCL (exact: the loss is a mean).
 """
 import argparse
-import gzip
 import os
-import pickle
 import random
 import sys
 import time
@@ -31,7 +30,7 @@ import yaml
 
 import iadmm_path  # noqa: F401
 from iadmm import data as qpdata
-from iadmm import ops, solver
+from iadmm import dataset, ops, solver
 
 
 def build_parser():
@@ -86,32 +85,50 @@ def split_ids(args):
 
 
 def load_qp_instances(args, ids, device):
-    """Reference on-disk format (main.py:621-722): one gzip-pickled dict per instance, Q doubled."""
-    path = os.path.join(args.data_dir, f"QP_{args.num_var}_{args.num_ineq}_{args.num_eq}")
-    keys = ("Q", "p", "A0", "zl", "zu", "G", "c", "A", "b")
-    cols = {k: [] for k in keys}
-    for i in ids:
-        with gzip.open(os.path.join(path, f"qp_{i}.gz"), "rb") as f:
-            d = pickle.load(f)  # user dataset in the reference's own format
-        for k in keys:
-            cols[k].append(d[k])
-    t = {k: torch.tensor(np.array(v), dtype=torch.float32, device=device) for k, v in cols.items()}
-    t["Q"] = t["Q"] * 2
-    return t
+    """Reference on-disk format (main.py:621-722, iadmm/dataset.py): one gzip-pickled dict per
+    instance, Q doubled; G/c, A/b optional."""
+    path = dataset.instance_dir(args.data_dir, args.num_var, args.num_ineq, args.num_eq, args.prob_type,
+                                args.qplib_num)
+    d = dataset.read_qp(path, ids, device, args.prob_type, args.qplib_num)
+    n, m = d["Q"].shape[1], d["A0"].shape[1]
+    mi = d["G"].shape[1] if "G" in d else 0
+    me = d["A"].shape[1] if "A" in d else 0
+    if mi + me != m:
+        raise SystemExit(f"{path}: A0 has {m} rows but G/A give {mi}+{me}; rows outside [G; A] are not supported")
+    if (args.num_var, args.num_ineq, args.num_eq) != (n, mi, me):  # sizes come from the data (main.py:656-690)
+        args.num_var, args.num_ineq, args.num_eq = n, mi, me
+    return d
 
 
 def checkpoint_path(args, model_name="lstm"):
-    # main.py:557-561 (test side reads QP_{n}_{eq}_{ineq}_{T}_{h})
-    return os.path.join(args.save_dir, model_name, "params",
-                        f"QP_{args.num_var}_{args.num_eq}_{args.num_ineq}_{args.outer_T}_{args.hidden_dim}.pth")
+    """main.py:78-165 save paths (test side main.py:557-612 reads QP_{n}_{eq}_{ineq}_...)."""
+    pt, T, h = args.prob_type, args.outer_T, args.hidden_dim
+    if pt in ("QP", "QP_RHS"):
+        name = f"{pt}_{args.num_var}_{args.num_eq}_{args.num_ineq}_{T}_{h}.pth"
+    elif pt in ("Random_QP", "SVM"):
+        name = f"{pt}_{args.num_var}_{args.num_ineq}_{T}_{h}.pth"
+    elif pt == "Equality_QP":
+        name = f"{pt}_{args.num_var}_{args.num_eq}_{T}_{h}.pth"
+    elif pt == "QPLIB":
+        name = f"{pt}_{args.qplib_num}_{T}_{h}.pth"
+    else:
+        name = f"{pt}_{T}_{h}.pth"
+    return os.path.join(args.save_dir, model_name, "params", name)
 
 
 def run_test(args):
     from models.lstm import LSTM
-    if args.prob_type != "QP":
-        raise SystemExit(f"prob_type {args.prob_type!r} is out of scope (DESIGN.md §0); use QP")
+    if args.prob_type not in dataset.LAYOUTS or (args.synthetic and args.prob_type != "QP"):
+        raise SystemExit(f"prob_type {args.prob_type!r}: datasets of {sorted(dataset.LAYOUTS)}; --synthetic is QP only")
     device = args.device or "cuda:0"
     torch.cuda.set_device(torch.device(device))
+    _, _, test_ids = split_ids(args)
+    tb = args.test_batch_size
+    nb = len(test_ids) // tb
+    if args.synthetic:
+        allq = None
+    else:  # load first: the sizes of non-QP types come from the data
+        allq = load_qp_instances(args, test_ids[:nb * tb], device)
     mi, me, n = args.num_ineq, args.num_eq, args.num_var
     model = LSTM(mi + me, args.input_dim, args.hidden_dim, args.outer_T, device)
     ck = checkpoint_path(args, model.name())
@@ -120,9 +137,6 @@ def run_test(args):
     elif not args.random_init:
         raise SystemExit(f"no checkpoint at {ck} (pass --random_init to run with random weights)")
     model.eval()
-    _, _, test_ids = split_ids(args)
-    tb = args.test_batch_size
-    nb = len(test_ids) // tb
     T = args.test_outer_T
     packed = solver.PackedWeights()
     reports, total_time, last = [], 0.0, None
@@ -130,12 +144,12 @@ def run_test(args):
         if args.synthetic:
             allq = qpdata.make_qp_batch(n, mi, me, nb * tb, first_index=0, seed=args.seed, device=device)
             allq.update(G=allq["A0"][:, :mi], A=allq["A0"][:, mi:], c=allq["zu"][:, :mi], b=allq["zu"][:, mi:])
-        else:
-            allq = load_qp_instances(args, test_ids[:nb * tb], device)
         for bi in range(nb):
             sl = slice(bi * tb, (bi + 1) * tb)
             d = {k: v[sl].contiguous() for k, v in allq.items()}
-            G, c, A, b = d["G"], d["c"].reshape(tb, -1), d["A"], d["b"].reshape(tb, -1)
+            G, A = d.get("G"), d.get("A")
+            c = d["c"].reshape(tb, -1) if mi else None
+            b = d["b"].reshape(tb, -1) if me else None
             viol = torch.zeros(4, T, tb, device=device)
 
             def hook(t, x, y, z):  # main.py:959-968, kept on the device
