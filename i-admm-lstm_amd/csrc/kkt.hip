@@ -9,6 +9,10 @@
 namespace iadmm {
 
 constexpr int kKktThreads = 256;
+// Column panel of the KKT sweeps: NG <= 8 float4 groups per lane (<= 2048 columns), so a lane
+// holds at most 32 row values + 32 column accumulators whatever n is (NG 16/24 needed 212-256
+// VGPRs and ran one wave per SIMD at n = 5000).
+constexpr int kPanelNG = 8;
 
 struct KktArgs {
   int n, m, num_ineq;
@@ -20,8 +24,11 @@ struct KktArgs {
 
 // One workgroup = one instance.  LDS: xs[n] (x~ -> r1), vs[m] (v -> r2), t1[n], t3[m], red[n].
 // PASS2=false stops after r and writes ||r||_2 (ls_res); PASS2=true computes g.
-template <int NG, bool VEC, bool PASS2>
-__global__ __launch_bounds__(kKktThreads) void kkt_kernel(KktArgs a) {
+// Columns are processed in panels of NG*256 (one panel when n <= NG*256); NT threads per
+// workgroup is chosen by the launcher so that large instances (whose LDS allows only one or two
+// workgroups per CU) still run 4 waves per SIMD.
+template <int NG, bool VEC, bool PASS2, int NT>
+__global__ __launch_bounds__(NT) void kkt_kernel(KktArgs a) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   const int n = a.n, m = a.m, N = n + m;
   float* xs = sm;
@@ -44,12 +51,25 @@ __global__ __launch_bounds__(kKktThreads) void kkt_kernel(KktArgs a) {
   const float irho_in = a.scal[IADMM_S_IRHO_IN], irho_eq = a.scal[IADMM_S_IRHO_EQ];
 
   // ---- pass 1: t1 = Q x~, t3 = A0 x~, red = A0^T v  (one read of Q and of A0)
+  constexpr int PW = NG * 256;
   float col[NG * 4];
+  if constexpr (NG < kPanelNG) {  // n <= PW: one panel, no panel loop (keeps the VGPR count low)
 #pragma unroll
-  for (int i = 0; i < NG * 4; ++i) col[i] = 0.f;
-  sweep<NG, VEC, true, false>(Qb, n, n, xs, nullptr, t1, col, wave, nw, lane);
-  if (m > 0) sweep<NG, VEC, true, true>(Ab, m, n, xs, vs, t3, col, wave, nw, lane);
-  col_reduce<NG, VEC>(col, red, n, wave, nw, lane);
+    for (int i = 0; i < NG * 4; ++i) col[i] = 0.f;
+    sweep<NG, VEC, true, false>(Qb, n, n, xs, nullptr, t1, col, wave, nw, lane);
+    if (m > 0) sweep<NG, VEC, true, true>(Ab, m, n, xs, vs, t3, col, wave, nw, lane);
+    col_reduce<NG, VEC>(col, red, n, wave, nw, lane);
+  } else {
+#pragma unroll 1
+    for (int c0 = 0; c0 < n; c0 += PW) {
+      const int cp = n - c0 < PW ? n - c0 : PW;
+#pragma unroll
+      for (int i = 0; i < NG * 4; ++i) col[i] = 0.f;
+      sweep_panel<NG, VEC, true, false>(Qb + c0, n, cp, n, xs + c0, nullptr, t1, c0 > 0, col, wave, nw, lane);
+      if (m > 0) sweep_panel<NG, VEC, true, true>(Ab + c0, m, cp, n, xs + c0, vs, t3, c0 > 0, col, wave, nw, lane);
+      col_reduce<NG, VEC>(col, red + c0, cp, wave, nw, lane);
+    }
+  }
 
   // ---- r = K xv - b~ (row i < n: (Q+sI) x~ + A0^T v - (s x - p); row n+j: A0 x~ - v/rho - (z - y/rho))
   float ss = 0.f;
@@ -77,11 +97,23 @@ __global__ __launch_bounds__(kKktThreads) void kkt_kernel(KktArgs a) {
   } else {
     __syncthreads();
     // ---- pass 2: red = Q^T r1 + A0^T r2 (one column accumulator), t3 = A0 r1
+    if constexpr (NG < kPanelNG) {
 #pragma unroll
-    for (int i = 0; i < NG * 4; ++i) col[i] = 0.f;
-    sweep<NG, VEC, false, true>(Qb, n, n, nullptr, xs, nullptr, col, wave, nw, lane);
-    if (m > 0) sweep<NG, VEC, true, true>(Ab, m, n, xs, vs, t3, col, wave, nw, lane);
-    col_reduce<NG, VEC>(col, red, n, wave, nw, lane);
+      for (int i = 0; i < NG * 4; ++i) col[i] = 0.f;
+      sweep<NG, VEC, false, true>(Qb, n, n, nullptr, xs, nullptr, col, wave, nw, lane);
+      if (m > 0) sweep<NG, VEC, true, true>(Ab, m, n, xs, vs, t3, col, wave, nw, lane);
+      col_reduce<NG, VEC>(col, red, n, wave, nw, lane);
+    } else {
+#pragma unroll 1
+      for (int c0 = 0; c0 < n; c0 += PW) {
+        const int cp = n - c0 < PW ? n - c0 : PW;
+#pragma unroll
+        for (int i = 0; i < NG * 4; ++i) col[i] = 0.f;
+        sweep_panel<NG, VEC, false, true>(Qb + c0, n, cp, n, nullptr, xs, nullptr, false, col, wave, nw, lane);
+        if (m > 0) sweep_panel<NG, VEC, true, true>(Ab + c0, m, cp, n, xs + c0, vs, t3, c0 > 0, col, wave, nw, lane);
+        col_reduce<NG, VEC>(col, red + c0, cp, wave, nw, lane);
+      }
+    }
     for (int i = tid; i < n; i += blockDim.x) a.g[b * N + i] = red[i] + sigma * xs[i];
     for (int j = tid; j < m; j += blockDim.x) {
       const float irho = j < a.num_ineq ? irho_in : irho_eq;
@@ -247,16 +279,32 @@ __global__ void kkt_assemble_kernel(int64_t B, int n, int m, int num_ineq, const
 
 inline bool kkt_fits(int64_t n, int64_t m) { return 3 * n + 2 * m <= 40960; }
 
-template <bool PASS2>
-int launch_kkt(int64_t B, int64_t n, int64_t m, KktArgs a, hipStream_t s) {
-  const int ng = ng_for(n);
-  const bool vec = (n % 4 == 0) && aligned16(a.Q) && (m == 0 || aligned16(a.A0));
-  const size_t lds = (3 * n + 2 * m) * sizeof(float);
-  IADMM_DISPATCH_NG(ng, vec, {
-    IADMM_ALLOW_LDS((kkt_kernel<NG_, V_, PASS2>), lds); hipLaunchKernelGGL((kkt_kernel<NG_, V_, PASS2>), dim3((unsigned)B), dim3(kKktThreads), lds, s, a);
-  });
+template <int NG, bool VEC, bool PASS2, int NT>
+int launch_kkt_nt(int64_t B, size_t lds, KktArgs a, hipStream_t s) {
+  IADMM_ALLOW_LDS((kkt_kernel<NG, VEC, PASS2, NT>), lds);
+  hipLaunchKernelGGL((kkt_kernel<NG, VEC, PASS2, NT>), dim3((unsigned)B), dim3(NT), lds, s, a);
   IADMM_CHECK_LAUNCH();
   return 0;
+}
+
+template <bool PASS2>
+int launch_kkt(int64_t B, int64_t n, int64_t m, KktArgs a, hipStream_t s) {
+  const int ng = ng_for(n < kPanelNG * 256 ? n : kPanelNG * 256);
+  const bool vec = (n % 4 == 0) && aligned16(a.Q) && (m == 0 || aligned16(a.A0));
+  const size_t lds = (3 * n + 2 * m) * sizeof(float);
+  // Workgroups per CU allowed by LDS (160 KiB): >= 4 -> 256 threads, else 512 (8 waves: at
+  // n = m = 5000, one 100 KB workgroup per CU, 512 threads measured 6.18 TB/s against 5.98 with
+  // 1024 (VGPR-capped, spills) and 5.55 with 256; tools/kktbench.py).
+  const size_t per_cu = (160 * 1024) / (lds > 0 ? lds : 1);
+  if (ng == 1) return vec ? launch_kkt_nt<1, true, PASS2, 256>(B, lds, a, s) : launch_kkt_nt<1, false, PASS2, 256>(B, lds, a, s);
+  if (ng == 2) return vec ? launch_kkt_nt<2, true, PASS2, 256>(B, lds, a, s) : launch_kkt_nt<2, false, PASS2, 256>(B, lds, a, s);
+  if (ng == 4) return vec ? launch_kkt_nt<4, true, PASS2, 256>(B, lds, a, s) : launch_kkt_nt<4, false, PASS2, 256>(B, lds, a, s);
+  if (per_cu >= 4) {
+    if (vec) return launch_kkt_nt<kPanelNG, true, PASS2, 256>(B, lds, a, s);
+    return launch_kkt_nt<kPanelNG, false, PASS2, 256>(B, lds, a, s);
+  }
+  if (vec) return launch_kkt_nt<kPanelNG, true, PASS2, 512>(B, lds, a, s);
+  return launch_kkt_nt<kPanelNG, false, PASS2, 512>(B, lds, a, s);
 }
 
 }  // namespace iadmm

@@ -41,11 +41,14 @@ IADMM_DEV void load_row(const float* __restrict__ row, bool rok, int C, int lane
   }
 }
 
-// DOT/COL sweep; see the file comment.  ``col`` accumulates in place.
+// DOT/COL sweep over a column panel: rows r < R of the [R x C] panel starting at Mx with row
+// stride ld (ld == C for a whole matrix); see the file comment.  ``col`` accumulates in place.
+// dot_acc: dot_s[r] += (panel dot) instead of =, so DOT over several panels sums them in panel
+// order (each row is always handled by the same wave, so no barrier is needed between panels).
 template <int NG, bool VEC, bool DOT, bool COL>
-IADMM_DEV void sweep(const float* __restrict__ Mx, int R, int C, const float* a_s,
-                     const float* c_s, float* dot_s, float (&col)[NG * 4], int wave, int nw,
-                     int lane) {
+IADMM_DEV void sweep_panel(const float* __restrict__ Mx, int R, int C, int64_t ld, const float* a_s,
+                           const float* c_s, float* dot_s, bool dot_acc, float (&col)[NG * 4],
+                           int wave, int nw, int lane) {
   constexpr bool HOIST = NG <= 8;
   constexpr int U = NG <= 4 ? 2 : 1;
   float av[HOIST ? NG * 4 : 1];
@@ -61,7 +64,7 @@ IADMM_DEV void sweep(const float* __restrict__ Mx, int R, int C, const float* a_
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int r = r0 + u;
-      load_row<NG, VEC>(Mx + (size_t)r * C, r < R, C, lane, v[u]);
+      load_row<NG, VEC>(Mx + (size_t)r * ld, r < R, C, lane, v[u]);
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -81,10 +84,17 @@ IADMM_DEV void sweep(const float* __restrict__ Mx, int R, int C, const float* a_
           d = fmaf(v[u][idx], a, d);
         }
         d = wave_sum(d);
-        if (lane == 0 && r < R) dot_s[r] = d;
+        if (lane == 0 && r < R) dot_s[r] = dot_acc ? dot_s[r] + d : d;
       }
     }
   }
+}
+
+template <int NG, bool VEC, bool DOT, bool COL>
+IADMM_DEV void sweep(const float* __restrict__ Mx, int R, int C, const float* a_s,
+                     const float* c_s, float* dot_s, float (&col)[NG * 4], int wave, int nw,
+                     int lane) {
+  sweep_panel<NG, VEC, DOT, COL>(Mx, R, C, C, a_s, c_s, dot_s, false, col, wave, nw, lane);
 }
 
 // Fold the per-wave column accumulators: red_s[c] = ((col_w0 + col_w1) + col_w2) + ...
