@@ -140,6 +140,9 @@ __global__ __launch_bounds__(256, 2) void gemm_tn_kernel(int64_t M, int Ni, int 
 #pragma unroll
       for (int q = 0; q < 16; ++q) acc[a][c][q] = 0.f;
   const bool vx = (Ni % 4 == 0) && aligned16(X), vy = (No % 4 == 0) && aligned16(Y);
+  // Loads are not register-prefetched: at 102 VGPRs four workgroups share a CU and hide each
+  // other's load latency (a prefetching variant needed 139 VGPRs, ran 3 per CU and was 30 %
+  // slower; tools/gemmbench.py).
   for (int64_t rc = rbeg; rc < rend; rc += kGBK) {
     __syncthreads();
 #pragma unroll
@@ -182,6 +185,60 @@ __global__ __launch_bounds__(256, 2) void gemm_tn_kernel(int64_t M, int Ni, int 
         const int o = o0 + wo + c * 32 + jl;
         if (i < Ni && o < No) S[(int64_t)i * No + o] = acc[a][c][q];
       }
+}
+
+// Skinny X^T Y (Ni <= 4, e.g. the [xv, g, 1]^T dP bias/input-weight gradient): a streaming
+// kernel that reads Y once (HBM-bound; the 128x128 MFMA tile would do 32-128x redundant work).
+// slab[s][i][c] = sum over rows of split s of X[r][i] * Y[r][c]; thread = 4 adjacent columns.
+template <int NI, bool VEC>
+__global__ __launch_bounds__(256) void gemm_tn_skinny_kernel(int64_t M, int No, int64_t rps, const float* X,
+                                                             const float* Y, float* slab) {
+  const int64_t sp = blockIdx.y;
+  const int c = (blockIdx.x * 256 + threadIdx.x) * 4;
+  if (c >= No) return;  // no barrier in this kernel
+  const int64_t r0 = sp * rps, r1 = (r0 + rps < M) ? r0 + rps : M;
+  float acc[NI][4];
+#pragma unroll
+  for (int i = 0; i < NI; ++i)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) acc[i][e] = 0.f;
+#pragma unroll 4
+  for (int64_t r = r0; r < r1; ++r) {
+    float4 y;
+    if constexpr (VEC) {
+      y = *reinterpret_cast<const float4*>(Y + r * No + c);
+    } else {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) set4(y, e, c + e < No ? Y[r * No + c + e] : 0.f);
+    }
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      const float xi = X[r * NI + i];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) acc[i][e] = fmaf(xi, get4(y, e), acc[i][e]);
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < NI; ++i) {
+    float* o = slab + (sp * NI + i) * (int64_t)No + c;
+    if constexpr (VEC) {
+      *reinterpret_cast<float4*>(o) = make_float4(acc[i][0], acc[i][1], acc[i][2], acc[i][3]);
+    } else {
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        if (c + e < No) o[e] = acc[i][e];
+    }
+  }
+}
+
+template <int NI>
+void launch_skinny(int64_t M, int No, int64_t rps, int64_t ns, const float* X, const float* Y, float* slab,
+                   hipStream_t s) {
+  const dim3 grid((unsigned)((No + 1023) / 1024), (unsigned)ns);
+  if (No % 4 == 0 && aligned16(Y) && aligned16(slab))
+    hipLaunchKernelGGL((gemm_tn_skinny_kernel<NI, true>), grid, dim3(256), 0, s, M, No, rps, X, Y, slab);
+  else
+    hipLaunchKernelGGL((gemm_tn_skinny_kernel<NI, false>), grid, dim3(256), 0, s, M, No, rps, X, Y, slab);
 }
 
 // out[e] (+)= sum_{s < nsplit} slab[s][e]  (fixed order)
@@ -227,8 +284,16 @@ extern "C" int iadmm_gemm_tn(int64_t M, int64_t Ni, int64_t No, int64_t rows_per
   const int64_t ns = (M + rows_per_split - 1) / rows_per_split;
   if (ns > 65535 || Ni > (1 << 20) || No > (1 << 20)) return IADMM_E_SIZE;
   hipStream_t s = (hipStream_t)stream;
-  const dim3 grid((unsigned)((Ni + 127) / 128), (unsigned)((No + 127) / 128), (unsigned)ns);
-  hipLaunchKernelGGL(gemm_tn_kernel, grid, dim3(256), 0, s, M, (int)Ni, (int)No, rows_per_split, X, Y, slab);
+  switch (Ni) {
+    case 1: launch_skinny<1>(M, (int)No, rows_per_split, ns, X, Y, slab, s); break;
+    case 2: launch_skinny<2>(M, (int)No, rows_per_split, ns, X, Y, slab, s); break;
+    case 3: launch_skinny<3>(M, (int)No, rows_per_split, ns, X, Y, slab, s); break;
+    case 4: launch_skinny<4>(M, (int)No, rows_per_split, ns, X, Y, slab, s); break;
+    default: {
+      const dim3 grid((unsigned)((Ni + 127) / 128), (unsigned)((No + 127) / 128), (unsigned)ns);
+      hipLaunchKernelGGL(gemm_tn_kernel, grid, dim3(256), 0, s, M, (int)Ni, (int)No, rows_per_split, X, Y, slab);
+    }
+  }
   IADMM_CHECK_LAUNCH();
   const int64_t nelem = Ni * No;
   const int64_t blocks = (nelem + 255) / 256;

@@ -150,15 +150,33 @@ __global__ __launch_bounds__(256, 2) void lstm_cell_bwd_kernel(CellBwdArgs a) {
 #pragma unroll
     for (int qq = 0; qq < 4; ++qq) {
       const int jj0 = 8 * qq + 4 * hf;
+      const int j0 = jt * kJT + jj0;
+      const int64_t o0 = R * h + j0;
+      // C, dH', dC' of the lane's 4 adjacent hidden units (16-B loads when h % 4 == 0)
+      float4 cin4, dh4, dc4;
+      const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+      if constexpr (VEC) {
+        const bool ok4 = rok && j0 < h;
+        cin4 = ok4 ? *reinterpret_cast<const float4*>(a.C + o0) : z4;
+        dh4 = (ok4 && a.dHn) ? *reinterpret_cast<const float4*>(a.dHn + o0) : z4;
+        dc4 = (ok4 && a.dCn) ? *reinterpret_cast<const float4*>(a.dCn + o0) : z4;
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const bool ok = rok && j0 + e < h;
+          set4(cin4, e, ok ? a.C[o0 + e] : 0.f);
+          set4(dh4, e, (ok && a.dHn) ? a.dHn[o0 + e] : 0.f);
+          set4(dc4, e, (ok && a.dCn) ? a.dCn[o0 + e] : 0.f);
+        }
+      }
       float4 wv[13];
 #pragma unroll
       for (int f = 0; f < 13; ++f) wv[f] = *reinterpret_cast<const float4*>(&sW[f * kJT + jj0]);
+      float4 dC4, dP4[4];
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const int q = qq * 4 + e;
-        const int j = jt * kJT + jj0 + e;
-        const bool ok = rok && j < h;
-        const int64_t o = R * h + j;
+        const bool ok = rok && j0 + e < h;
         float pre[4];
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
@@ -167,24 +185,40 @@ __global__ __launch_bounds__(256, 2) void lstm_cell_bwd_kernel(CellBwdArgs a) {
         }
         const float ig = sigmoidf_(pre[0]), fg = sigmoidf_(pre[1]), og = sigmoidf_(pre[2]);
         const float ug = tanhf(pre[3]);
-        const float cin = ok ? a.C[o] : 0.f;
+        const float cin = get4(cin4, e);
         const float c2 = ig * ug + fg * cin;
         const float tc = tanhf(c2);
         const float h2 = og * tc;
         const float wh = get4(wv[12], e);
-        const float dHt = (ok && a.dHn ? a.dHn[o] : 0.f) + dq * wh;
+        const float dHt = get4(dh4, e) + dq * wh;
         const float dO = dHt * tc;
-        const float dCt = (ok && a.dCn ? a.dCn[o] : 0.f) + dHt * og * (1.f - tc * tc);
+        const float dCt = get4(dc4, e) + dHt * og * (1.f - tc * tc);
         const float dI = dCt * ug, dU = dCt * ig, dF = dCt * cin;
         const float dPi = dI * ig * (1.f - ig), dPf = dF * fg * (1.f - fg);
         const float dPo = dO * og * (1.f - og), dPu = dU * (1.f - ug * ug);
+        set4(dC4, e, dCt * fg);
+        set4(dP4[0], e, dPi); set4(dP4[1], e, dPf); set4(dP4[2], e, dPo); set4(dP4[3], e, dPu);
         if (ok) {
-          a.dC[o] = dCt * fg;
-          float* dp = a.dP + R * (int64_t)(4 * h) + j;
-          dp[0] = dPi; dp[h] = dPf; dp[2 * h] = dPo; dp[3 * h] = dPu;
           whp[q] += h2 * dq;
           din0 += dPi * get4(wv[0], e) + dPf * get4(wv[3], e) + dPo * get4(wv[6], e) + dPu * get4(wv[9], e);
           din1 += dPi * get4(wv[1], e) + dPf * get4(wv[4], e) + dPo * get4(wv[7], e) + dPu * get4(wv[10], e);
+        }
+      }
+      float* dp = a.dP + R * (int64_t)(4 * h) + j0;
+      if constexpr (VEC) {
+        if (rok && j0 < h) {
+          *reinterpret_cast<float4*>(a.dC + o0) = dC4;
+#pragma unroll
+          for (int g = 0; g < 4; ++g) *reinterpret_cast<float4*>(dp + g * h) = dP4[g];
+        }
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          if (rok && j0 + e < h) {
+            a.dC[o0 + e] = get4(dC4, e);
+#pragma unroll
+            for (int g = 0; g < 4; ++g) dp[g * h + e] = get4(dP4[g], e);
+          }
         }
       }
     }
@@ -421,7 +455,8 @@ extern "C" int iadmm_lstm_cell_bwd(int64_t M, int64_t h, const float* H, const f
   if (nrt * njt > 0x7fffffffLL || h > (1 << 16)) return IADMM_E_SIZE;
   CellBwdArgs a{M, (int)h, (int)njt, (int)((h + kBK - 1) / kBK), (int)nrt, H, C, xv, g, Upk, Wx, dq, dHn, dCn,
                 dC, dP, whslab, inpart};
-  const bool vec = (h % 4 == 0) && aligned16(H);
+  const bool vec = (h % 4 == 0) && aligned16(H) && aligned16(C) && aligned16(dC) && aligned16(dP) &&
+                   (!dHn || aligned16(dHn)) && (!dCn || aligned16(dCn));
   const dim3 grid((unsigned)(nrt * njt));
   if (vec) hipLaunchKernelGGL(lstm_cell_bwd_kernel<true>, grid, dim3(256), 0, (hipStream_t)stream, a);
   else hipLaunchKernelGGL(lstm_cell_bwd_kernel<false>, grid, dim3(256), 0, (hipStream_t)stream, a);

@@ -66,7 +66,7 @@ class IterationFn(torch.autograd.Function):
         dH = ops.gemm_nt(dP, Ucat).reshape(H.shape)
         dUcat = ops.gemm_tn(H.reshape(M, h), dP)
         X3 = torch.stack([xv.reshape(M), g.reshape(M), torch.ones(M, device=x.device)], dim=1).contiguous()
-        dW3 = ops.gemm_tn(X3, dP)                                                     # [3, 4h]
+        dW3 = ops.gemm_tn(X3, dP, rows_per_split=512)                                 # [3, 4h], streaming
         dWh = ops.slab_reduce(whslab).reshape(h, 1)
         # 4. d(in) -> d(xv), dg ; 5. KKT backward
         dg = ops.in_reduce(inpart, dxv)

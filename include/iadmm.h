@@ -185,7 +185,8 @@ int iadmm_gemm_nt(int64_t M, int64_t Ni, int64_t K, const float* X, const float*
                   int accumulate, void* stream);
 
 /* out[Ni,No] (+)= X[M,Ni]^T . Y[M,No], split over M in slices of rows_per_split (multiple of 32):
- * slab[iadmm_gemm_tn_splits(M, rows_per_split)][Ni][No] is caller-owned scratch. */
+ * slab[iadmm_gemm_tn_splits(M, rows_per_split)][Ni][No] is caller-owned scratch.  fp32 MFMA for
+ * Ni > 4 (dU_cat = H^T dP); Ni <= 4 (d[W_x; b] = [xv, g, 1]^T dP) streams Y once on the VALU. */
 int64_t iadmm_gemm_tn_splits(int64_t M, int64_t rows_per_split);
 int iadmm_gemm_tn(int64_t M, int64_t Ni, int64_t No, int64_t rows_per_split, const float* X,
                   const float* Y, float* slab, float* out, int accumulate, void* stream);
