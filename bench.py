@@ -196,7 +196,7 @@ def main():
                                 "algorithmic_per_launch": kkt_bytes},
             "phase_ms_per_step": {k: v / args.steps for k, v in spans.items() if not k.startswith("k:")},
         }
-        if args.cpu_sample > 0:
+        if args.cpu_sample > 0 and world == 1:  # the CPU baseline is an N=1 figure
             res["cpu_baseline"] = cpu_baseline(args, d if keep else master, params)
         print(json.dumps(res), flush=True)
     if dist:

@@ -42,41 +42,42 @@ IADMM_DEV void cell_mainloop(const float* __restrict__ H, int64_t M, int h, int 
 #pragma unroll
       for (int q = 0; q < 16; ++q) acc[g][r][q] = 0.f;
 
-  float4 ra[4], rb[8];
+  // Staging registers as named scalars (an array here was turned into an LDS/scratch alloca
+  // by the compiler, which then waited for each global load right after issuing it).
+  float4 ra0, ra1, ra2, ra3, rb0, rb1, rb2, rb3, rb4, rb5, rb6, rb7;
+  auto ldB = [&](int kc, int i) -> float4 {
+    const int idx = tid + 256 * i, row = idx >> 3, c4 = idx & 7;
+    const int64_t R = rbase + row;
+    const int k = kc * kBK + c4 * 4;
+    if constexpr (VEC) {
+      return (R < M && k < h) ? *reinterpret_cast<const float4*>(H + R * h + k) : make_float4(0.f, 0.f, 0.f, 0.f);
+    } else {
+      float4 t;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) set4(t, e, (R < M && k + e < h) ? H[R * h + k + e] : 0.f);
+      return t;
+    }
+  };
   auto gload = [&](int kc) {
     const float4* Ac = reinterpret_cast<const float4*>(Ubase + (int64_t)kc * 128 * kBK);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) ra[i] = Ac[tid + 256 * i];
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int idx = tid + 256 * i, row = idx >> 3, c4 = idx & 7;
-      const int64_t R = rbase + row;
-      const int k = kc * kBK + c4 * 4;
-      if constexpr (VEC) {
-        rb[i] = (R < M && k < h) ? *reinterpret_cast<const float4*>(H + R * h + k)
-                                 : make_float4(0.f, 0.f, 0.f, 0.f);
-      } else {
-        float4 t;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) set4(t, e, (R < M && k + e < h) ? H[R * h + k + e] : 0.f);
-        rb[i] = t;
-      }
-    }
+    ra0 = Ac[tid];
+    ra1 = Ac[tid + 256];
+    ra2 = Ac[tid + 512];
+    ra3 = Ac[tid + 768];
+    rb0 = ldB(kc, 0); rb1 = ldB(kc, 1); rb2 = ldB(kc, 2); rb3 = ldB(kc, 3);
+    rb4 = ldB(kc, 4); rb5 = ldB(kc, 5); rb6 = ldB(kc, 6); rb7 = ldB(kc, 7);
+  };
+  auto st = [&](float* sm, int i, const float4& v) {
+    const int idx = tid + 256 * i, row = idx >> 3, c4 = idx & 7;
+    *reinterpret_cast<float4*>(&sm[row * kLD + c4 * 4]) = v;
   };
 
   gload(0);
   for (int kc = 0; kc < nkc; ++kc) {
     __syncthreads();
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int idx = tid + 256 * i, row = idx >> 3, c4 = idx & 7;
-      *reinterpret_cast<float4*>(&sA[row * kLD + c4 * 4]) = ra[i];
-    }
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int idx = tid + 256 * i, row = idx >> 3, c4 = idx & 7;
-      *reinterpret_cast<float4*>(&sB[row * kLD + c4 * 4]) = rb[i];
-    }
+    st(sA, 0, ra0); st(sA, 1, ra1); st(sA, 2, ra2); st(sA, 3, ra3);
+    st(sB, 0, rb0); st(sB, 1, rb1); st(sB, 2, rb2); st(sB, 3, rb3);
+    st(sB, 4, rb4); st(sB, 5, rb5); st(sB, 6, rb6); st(sB, 7, rb7);
     __syncthreads();
     if (kc + 1 < nkc) gload(kc + 1);
 #pragma unroll
