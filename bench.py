@@ -66,7 +66,9 @@ def pmc_traffic(kernel_prefix, n, m, h, B):
         files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_pmc_{ctr}_n{n}_m{m}_h{h}_B{B}.csv")))
         if not files:
             return None
-        rows = [r for r in csv.DictReader(open(files[-1])) if kernel_prefix in r["kernel"] and r["counter"] == ctr]
+        names = (kernel_prefix,) if isinstance(kernel_prefix, str) else kernel_prefix
+        rows = [r for r in csv.DictReader(open(files[-1]))
+                if any(k in r["kernel"] for k in names) and r["counter"] == ctr]
         if not rows:
             return None
         tot += mult * float(rows[0]["mean"]) * 1024.0
@@ -185,7 +187,7 @@ def main():
             "final_residual": {"primal_mean": primal, "dual_mean": dual, "sum": primal + dual},
             "roofline": {"kernel": "iadmm_lstm_cell_fwd", "bound": "mfma", "achieved": cell_tf,
                          "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": cell_tf / FP32_MFMA_PEAK_TFLOPS,
-                         "traffic": pmc_traffic("lstm_cell_kernel", n, mi + me, h, B),
+                         "traffic": pmc_traffic(("cell_fwd_kernel<", "lstm_cell_kernel"), n, mi + me, h, B),
                          "traffic_source": "profiles/r*_pmc_{FETCH,WRITE}_SIZE_*.csv (separate --pmc passes)",
                          "avg_launch_ms": ms_cell, "launches": n_cell,
                          "algorithmic_per_launch": cell_flop},

@@ -61,101 +61,6 @@ __global__ void lstm_pack_wx_kernel(int h, int hp, WxSrc s, float* Wx) {
   }
 }
 
-struct CellArgs {
-  int64_t M;
-  int h, njt, nkc, nrt;
-  const float *H, *C, *xv, *g, *Upk, *Wx;
-  float *Hn, *Cn, *part;
-};
-
-template <bool VEC>
-__global__ __launch_bounds__(256, 2) void lstm_cell_kernel(CellArgs a) {
-  __shared__ __attribute__((aligned(16))) float sA[128 * kLD];
-  __shared__ __attribute__((aligned(16))) float sB[kRows * kLD];
-  __shared__ __attribute__((aligned(16))) float sW[kWxF * kJT];
-
-  int jt, rt;
-  cell_tile_of_block(a.njt, jt, rt);
-
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int jl = lane & 31, hf = lane >> 5;
-  const int h = a.h;
-  const int64_t M = a.M;
-  const int64_t rbase = (int64_t)rt * kRows;
-
-  for (int i = tid; i < kWxF * kJT; i += 256) {
-    const int f = i / kJT, jj = i % kJT;
-    sW[i] = a.Wx[(int64_t)(jt * kJT + jj) * kWxF + f];
-  }
-
-  floatx16 acc[4][2];
-  cell_mainloop<VEC>(a.H, M, h, a.nkc, a.Upk + (int64_t)jt * a.nkc * 128 * kBK, rbase, sA, sB, acc, tid,
-                     wave, jl, hf);
-
-  // ---- epilogue: gates, cell update, projection partial (all in registers)
-  // accumulator element q of lane (jl,hf): hidden jj = (q&3) + 8*(q>>2) + 4*hf, data row jl.
-#pragma unroll
-  for (int r = 0; r < 2; ++r) {
-    const int64_t R = rbase + wave * 64 + r * 32 + jl;
-    const bool rok = R < M;
-    const float in0 = rok ? a.xv[R] : 0.f;
-    const float in1 = rok ? a.g[R] : 0.f;
-    float gsum = 0.f;
-#pragma unroll
-    for (int qq = 0; qq < 4; ++qq) {
-      const int jj0 = 8 * qq + 4 * hf;
-      const int j0 = jt * kJT + jj0;
-      float4 cold;
-      if constexpr (VEC) {
-        cold = (rok && j0 < h) ? *reinterpret_cast<const float4*>(a.C + R * h + j0)
-                               : make_float4(0.f, 0.f, 0.f, 0.f);
-      } else {
-#pragma unroll
-        for (int e = 0; e < 4; ++e) set4(cold, e, (rok && j0 + e < h) ? a.C[R * h + j0 + e] : 0.f);
-      }
-      float4 wv[13];
-#pragma unroll
-      for (int f = 0; f < 13; ++f) wv[f] = *reinterpret_cast<const float4*>(&sW[f * kJT + jj0]);
-      float4 cnew, hnew;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int q = qq * 4 + e;
-        float pre[4];
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          const float xw = in0 * get4(wv[3 * g], e) + in1 * get4(wv[3 * g + 1], e);
-          pre[g] = (xw + acc[g][r][q]) + get4(wv[3 * g + 2], e);
-        }
-        const float ig = sigmoidf_(pre[0]), fg = sigmoidf_(pre[1]), og = sigmoidf_(pre[2]);
-        const float ug = tanhf(pre[3]);
-        const float c2 = ig * ug + fg * get4(cold, e);
-        const float h2 = og * tanhf(c2);
-        set4(cnew, e, c2);
-        set4(hnew, e, h2);
-        gsum = fmaf(h2, get4(wv[12], e), gsum);
-      }
-      if (rok) {
-        if constexpr (VEC) {
-          if (j0 < h) {
-            *reinterpret_cast<float4*>(a.Cn + R * h + j0) = cnew;
-            *reinterpret_cast<float4*>(a.Hn + R * h + j0) = hnew;
-          }
-        } else {
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            if (j0 + e < h) {
-              a.Cn[R * h + j0 + e] = get4(cnew, e);
-              a.Hn[R * h + j0 + e] = get4(hnew, e);
-            }
-          }
-        }
-      }
-    }
-    gsum += __shfl_xor(gsum, 32, 64);
-    if (hf == 0 && rok) a.part[(int64_t)jt * M + R] = gsum;
-  }
-}
-
 }  // namespace iadmm
 
 using namespace iadmm;
@@ -194,13 +99,13 @@ extern "C" int iadmm_lstm_cell_fwd(int64_t M, int64_t h, const float* H, const f
   if (!aligned16(Upk)) return IADMM_E_ALIGN;
   const int64_t nrt = cdiv(M, kRows), njt = cdiv(h, kJT);
   if (nrt * njt > 0x7fffffffLL || h > (1 << 16)) return IADMM_E_SIZE;
-  CellArgs a{M, (int)h, (int)njt, (int)cdiv(h, kBK), (int)nrt, H, C, xv, g, Upk, Wx, Hn, Cn, part};
+  CellArgsT a{M, (int)h, (int)njt, (int)cdiv(h, kBK), H, C, xv, g, Upk, Wx, Hn, Cn, part};
   const bool vec = (h % 4 == 0) && aligned16(H) && aligned16(C) && aligned16(Hn) && aligned16(Cn);
   const dim3 grid((unsigned)(nrt * njt));
   if (vec)
-    hipLaunchKernelGGL(lstm_cell_kernel<true>, grid, dim3(256), 0, (hipStream_t)stream, a);
+    hipLaunchKernelGGL((cell_fwd_kernel<true, 4, 0>), grid, dim3(256), 0, (hipStream_t)stream, a);
   else
-    hipLaunchKernelGGL(lstm_cell_kernel<false>, grid, dim3(256), 0, (hipStream_t)stream, a);
+    hipLaunchKernelGGL((cell_fwd_kernel<false, 4, 0>), grid, dim3(256), 0, (hipStream_t)stream, a);
   IADMM_CHECK_LAUNCH();
   return 0;
 }

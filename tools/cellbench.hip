@@ -1,8 +1,12 @@
 // Variant microbenchmark of the fused LSTM-cell kernel at the bench shape (M = 1024*2000 rows,
 // h = 800): interleaved rounds of every variant in one process (cdna_hip_programming.md §5.4
 // rule 24), hipEvent timing, TFLOP/s on the algorithmic 8*M*h^2 + 18*M*h flops.
-// Build: hipcc -O3 -std=c++17 --offload-arch=gfx950 -ffp-contract=off tools/cellbench.hip -o /tmp/cellbench
-#include "../i-admm-lstm_amd/csrc/cell_kernel.h"
+// Build: hipcc -O3 -std=c++17 --offload-arch=gfx950 -ffp-contract=off -mllvm -disable-promote-alloca-to-lds \
+//          tools/cellbench.hip -o tools/cellbench.bin
+// Variants are instances of the production kernel template (cell_tile.h cell_fwd_kernel<VEC, NW,
+// PRIO>); the first is the one lstm.hip launches.  Round-1 study of earlier variants (BK 16 / double
+// buffer / fast transcendentals / 16x16x4 MFMA): profiles/r01_cellbench.txt.
+#include "../i-admm-lstm_amd/csrc/cell_tile.h"
 
 #include <cstdio>
 #include <cstdlib>
@@ -40,6 +44,26 @@ __global__ __launch_bounds__(256, 2) void mfma_ceiling(int iters, float* out, fl
     float s = 0.f;
     for (int i = 0; i < 8; ++i) for (int q = 0; q < 16; ++q) s += acc[i][q];
     out[blockIdx.x * 256 + threadIdx.x] = s;
+  } else if constexpr (SHAPE == 33) {  // 32x32x2 with random full-mantissa operands, 64 pairings
+    float ar[8], br[8];
+    for (int i = 0; i < 8; ++i) {
+      uint32_t x = (uint32_t)(threadIdx.x * 8 + i + blockIdx.x * 4096) * 2654435761u;
+      x ^= x >> 13; x *= 0x5bd1e995u; x ^= x >> 15;
+      ar[i] = (x & 0xffffff) / 16777216.0f * 2.f - 1.f;
+      x = x * 2654435761u + 12345u; x ^= x >> 13; x *= 0x5bd1e995u; x ^= x >> 15;
+      br[i] = (x & 0xffffff) / 16777216.0f * 2.f - 1.f;
+    }
+    floatx16 acc[8];
+    for (int i = 0; i < 8; ++i) for (int q = 0; q < 16; ++q) acc[i][q] = 0.f;
+    for (int it = 0; it < iters; it += 8) {
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+#pragma unroll
+        for (int i = 0; i < 8; ++i) acc[i] = __builtin_amdgcn_mfma_f32_32x32x2f32(ar[i], br[(i + u) & 7], acc[i], 0, 0, 0);
+    }
+    float s = 0.f;
+    for (int i = 0; i < 8; ++i) for (int q = 0; q < 16; ++q) s += acc[i][q];
+    out[blockIdx.x * 256 + threadIdx.x] = s;
   } else {
     floatx4 acc[32];
     for (int i = 0; i < 32; ++i) for (int q = 0; q < 4; ++q) acc[i][q] = 0.f;
@@ -58,17 +82,11 @@ struct Variant {
   void (*launch)(CellArgsT, int64_t, hipStream_t);
 };
 
-template <int NW, int BK, bool DBUF, bool FAST, int EPI>
+template <int NW, int PRIO>
 void launch_v(CellArgsT a, int64_t M, hipStream_t s) {
   const int64_t rows = 64 * NW;
   const int64_t nrt = (M + rows - 1) / rows;
-  hipLaunchKernelGGL((cell_fwd_kernel<NW, BK, DBUF, FAST, EPI, true>), dim3((unsigned)(nrt * a.njt)), dim3(64 * NW), 0, s, a);
-}
-
-template <bool FAST, int EPI>
-void launch_16(CellArgsT a, int64_t M, hipStream_t s) {
-  const int64_t nrt = (M + 255) / 256;
-  hipLaunchKernelGGL((cell_fwd16_kernel<FAST, EPI>), dim3((unsigned)(nrt * a.njt)), dim3(256), 0, s, a);
+  hipLaunchKernelGGL((cell_fwd_kernel<true, NW, PRIO>), dim3((unsigned)(nrt * a.njt)), dim3(64 * NW), 0, s, a);
 }
 
 int main(int argc, char** argv) {
@@ -91,19 +109,11 @@ int main(int argc, char** argv) {
   CK(hipDeviceSynchronize());
   CellArgsT a{M, (int)h, njt, nkc32, H, C, xv, g, Upk, Wx, Hn, Cn, part};
   std::vector<Variant> vs = {
-      {"NW4 BK32 single  precise", launch_v<4, 32, false, false, 0>},
-      {"NW4 BK32 single  fast   ", launch_v<4, 32, false, true, 0>},
-      {"NW4 BK32 single  noepi  ", launch_v<4, 32, false, false, 1>},
-      {"NW4 BK16 dbuf    precise", launch_v<4, 16, true, false, 0>},
-      {"NW4 BK16 dbuf    fast   ", launch_v<4, 16, true, true, 0>},
-      {"NW4 BK16 dbuf    noepi  ", launch_v<4, 16, true, false, 1>},
-      {"NW8 BK16 dbuf    precise", launch_v<8, 16, true, false, 0>},
-      {"NW8 BK16 dbuf    fast   ", launch_v<8, 16, true, true, 0>},
-      {"NW8 BK16 dbuf    noepi  ", launch_v<8, 16, true, false, 1>},
-      {"NW8 BK32 single  precise", launch_v<8, 32, false, false, 0>},
-      {"16x16x4 BK32     precise", launch_16<false, 0>},
-      {"16x16x4 BK32     fast   ", launch_16<true, 0>},
-      {"16x16x4 BK32     noepi  ", launch_16<false, 1>},
+      {"NW4 (production)        ", launch_v<4, 0>},
+      {"NW4 setprio per cluster ", launch_v<4, 1>},
+      {"NW8                     ", launch_v<8, 0>},
+      {"NW8 setprio per cluster ", launch_v<8, 1>},
+      {"NW8 static prio waves4-7", launch_v<8, 2>},
   };
   const double flop = (8.0 * h * h + 18.0 * h) * M;
   hipStream_t s;
@@ -125,33 +135,37 @@ int main(int argc, char** argv) {
     }
   }
   CK(hipGetLastError());
-  {  // cross-check: 32x32x2 and 16x16x4 variants produce the same H', C', part (fp32 rounding)
-    std::vector<float> h1(1 << 20), h2(1 << 20), p1(1 << 18), p2(1 << 18);
-    launch_v<4, 32, false, false, 0>(a, M, s);
+  {  // cross-check: every variant must reproduce the production kernel bit for bit
+    std::vector<float> h1(1 << 22), h2(1 << 22), p1(1 << 20), p2(1 << 20);
+    vs[0].launch(a, M, s);
     CK(hipMemcpyAsync(h1.data(), Hn, h1.size() * 4, hipMemcpyDeviceToHost, s));
     CK(hipMemcpyAsync(p1.data(), part, p1.size() * 4, hipMemcpyDeviceToHost, s));
-    launch_16<false, 0>(a, M, s);
-    CK(hipMemcpyAsync(h2.data(), Hn, h2.size() * 4, hipMemcpyDeviceToHost, s));
-    CK(hipMemcpyAsync(p2.data(), part, p2.size() * 4, hipMemcpyDeviceToHost, s));
     CK(hipStreamSynchronize(s));
-    double dh = 0, nh = 0, dp = 0, np_ = 0;
-    for (size_t i = 0; i < h1.size(); ++i) { dh += (h1[i] - h2[i]) * (double)(h1[i] - h2[i]); nh += h1[i] * (double)h1[i]; }
-    for (size_t i = 0; i < p1.size(); ++i) { dp += (p1[i] - p2[i]) * (double)(p1[i] - p2[i]); np_ += p1[i] * (double)p1[i]; }
-    printf("cross-check 16x16 vs 32x32: rel-L2 H' %.3e  part %.3e\n", sqrt(dh / nh), sqrt(dp / np_));
+    for (size_t i = 1; i < vs.size(); ++i) {
+      vs[i].launch(a, M, s);
+      CK(hipMemcpyAsync(h2.data(), Hn, h2.size() * 4, hipMemcpyDeviceToHost, s));
+      CK(hipMemcpyAsync(p2.data(), part, p2.size() * 4, hipMemcpyDeviceToHost, s));
+      CK(hipStreamSynchronize(s));
+      size_t bad = 0;
+      for (size_t k = 0; k < h1.size(); ++k) bad += h1[k] != h2[k];
+      for (size_t k = 0; k < p1.size(); ++k) bad += p1[k] != p2[k];
+      printf("bitwise check %s: %zu mismatches\n", vs[i].name.c_str(), bad);
+    }
   }
   printf("M=%lld h=%lld rounds=%d\n", (long long)M, (long long)h, rounds);
   {  // MFMA ceiling: 512 blocks x 4 waves, each wave 8 x 32x32x2 (or 32 x 16x16x4) per iteration
     const int iters = 20000, blocks = 512;
-    for (int shape : {32, 16, 32, 16}) {
+    for (int shape : {32, 33, 32, 33}) {
       CK(hipEventRecord(e0, s));
       if (shape == 32) hipLaunchKernelGGL(mfma_ceiling<32>, dim3(blocks), dim3(256), 0, s, iters, part, 1e-3f);
-      else hipLaunchKernelGGL(mfma_ceiling<16>, dim3(blocks), dim3(256), 0, s, iters, part, 1e-3f);
+      else hipLaunchKernelGGL(mfma_ceiling<33>, dim3(blocks), dim3(256), 0, s, iters, part, 1e-3f);
       CK(hipEventRecord(e1, s));
       CK(hipEventSynchronize(e1));
       float ms;
       CK(hipEventElapsedTime(&ms, e0, e1));
-      const double f = (double)blocks * 4 * iters * 8 * 4096.0;  // both shapes: 32768 flop per wave-iteration
-      printf("MFMA ceiling %dx%d f32: %8.3f ms  %7.1f TFLOP/s\n", shape, shape, ms, f / (ms * 1e-3) / 1e12);
+      const double f = (double)blocks * 4 * iters * 8 * 4096.0;  // 8 MFMAs x 4096 flop per wave-iteration
+      printf("MFMA ceiling 32x32x2 f32, %s operands: %8.3f ms  %7.1f TFLOP/s\n",
+             shape == 32 ? "fixed small" : "random     ", ms, f / (ms * 1e-3) / 1e12);
     }
   }
   for (size_t i = 0; i < vs.size(); ++i) {
