@@ -107,8 +107,9 @@ def main():
     args = parse()
     from iadmm import data, parallel, solver
     world, rank, local = parallel.env()
+    local, backend = parallel.device_and_backend(local)
     torch.cuda.set_device(local)
-    dist = parallel.init("nccl", local) if world > 1 else None
+    dist = parallel.init(backend, local) if world > 1 else None
 
     n, mi, me, h, T, B = args.num_var, args.num_ineq, args.num_eq, args.hidden_dim, args.outer_T, args.batch
     N = n + mi + me

@@ -35,8 +35,9 @@ def main():
     from iadmm import data, ops, parallel, train
     from models.lstm import LSTM
     world, rank, local = parallel.env()
+    local, backend = parallel.device_and_backend(local)
     torch.cuda.set_device(local)
-    dist = parallel.init("nccl", local) if world > 1 else None
+    dist = parallel.init(backend, local) if world > 1 else None
     n, mi, me, h, T, B = args.num_var, args.num_ineq, args.num_eq, args.hidden_dim, args.outer_T, args.batch
     first, count = parallel.shard(world * B, world, rank)
     d = data.make_qp_batch(n, mi, me, count, first_index=first, device="cuda")

@@ -19,6 +19,19 @@ def env():
             int(os.environ.get("LOCAL_RANK", "0")))
 
 
+SHARED_GPU_ENV = "IADMM_SHARED_GPU"
+
+
+def device_and_backend(local_rank):
+    """(cuda device index, backend) of this rank: one GPU per rank over RCCL ("nccl").  With
+    IADMM_SHARED_GPU=1 every rank uses cuda:0 over gloo -- a rehearsal of the N>1 code path
+    (sharding, barriers, max-over-ranks, gradient all-reduce) on a one-GPU machine; RCCL refuses
+    two ranks on one device."""
+    if os.environ.get(SHARED_GPU_ENV) == "1":
+        return 0, "gloo"
+    return int(local_rank), "nccl"
+
+
 def shard(global_batch, world, rank):
     """Contiguous [start, start+count) of ``global_batch`` instances for ``rank`` (sizes differ by
     at most one when the batch does not divide)."""

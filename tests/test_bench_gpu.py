@@ -1,0 +1,74 @@
+"""bench.py / bench_train.py contract on the GPU: the one-line JSON of a single-GPU run, and the
+N > 1 code path (instance sharding, barriers, max-over-ranks timing, gradient all-reduce)
+rehearsed with two ranks sharing cuda:0 over gloo (IADMM_SHARED_GPU=1; RCCL refuses two ranks on
+one device).  Small shapes; the full-size numbers come from the round-end bench runs."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+SMALL = ["--num_var", "64", "--num_ineq", "32", "--num_eq", "32", "--hidden_dim", "64", "--outer_T", "3"]
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _run(args, nproc=1, timeout=600):
+    env = dict(os.environ)
+    if nproc > 1:
+        env["IADMM_SHARED_GPU"] = "1"
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
+               "--master-addr", "127.0.0.1", "--master-port", str(_free_port())] + args
+    else:
+        cmd = [sys.executable] + args
+    out = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=timeout)
+    assert out.returncode == 0, out.stderr[-3000:]
+    lines = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, out.stdout[-2000:]
+    return json.loads(lines[0])
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+
+
+def test_bench_single_gpu_contract():
+    r = _run(["bench.py", "--batch", "8", "--steps", "2", "--warmup", "1", "--cpu-sample", "2"] + SMALL)
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better",
+              "scaling", "vs_baseline", "dtype", "data", "config", "roofline", "cpu_baseline"):
+        assert k in r, k
+    assert r["n_gpus"] == 1 and r["steps"] == 2 and r["warmup"] == 1 and r["higher_is_better"] is True
+    assert r["value"] > 0 and r["config"]["global_batch"] == 8
+    rf = r["roofline"]
+    assert rf["bound"] == "mfma" and rf["unit"] == "TFLOP/s" and rf["launches"] == 2 * 3
+    assert abs(rf["frac"] - rf["achieved"] / rf["peak"]) < 1e-9
+    cb = r["cpu_baseline"]
+    assert cb["kind"] == "port" and cb["value"] > 0 and cb["cores"] >= 1
+    # the GPU and the CPU oracle solved the same instances: residuals of the same magnitude
+    assert r["final_residual"]["primal_mean"] > 0
+
+
+def test_bench_two_ranks_shared_gpu():
+    r = _run(["bench.py", "--batch", "4", "--steps", "1", "--warmup", "0", "--cpu-sample", "2"] + SMALL, nproc=2)
+    assert r["n_gpus"] == 2 and r["config"]["global_batch"] == 8 and r["scaling"] == "weak"
+    assert "cpu_baseline" not in r  # an N = 1 figure only
+    assert r["value"] > 0
+
+
+def test_bench_train_two_ranks_shared_gpu():
+    r = _run(["bench_train.py", "--batch", "2", "--micro_batch", "1", "--steps", "1", "--warmup", "0",
+              "--num_var", "32", "--num_ineq", "16", "--num_eq", "16", "--hidden_dim", "32", "--outer_T", "2"],
+             nproc=2)
+    assert r["n_gpus"] == 2 and r["value"] > 0 and r["loss"] == r["loss"]
