@@ -36,9 +36,20 @@ __global__ __launch_bounds__(kLuThreads) void lu_panel_kernel(int N, int k0, flo
   const int R = N - k0;
   const int nb = min(kNB, R);
 
-  for (int idx = tid; idx < R * nb; idx += blockDim.x) {
-    const int r = idx / nb, c = idx % nb;
-    P[r * kPS + c] = Ab[(size_t)(k0 + r) * N + k0 + c];
+  // 16-B loads when the panel is a whole 16-column block of 16-B-aligned rows
+  const bool vec = nb == kNB && (N % 4) == 0 && aligned16(Ab);
+  if (vec) {
+#pragma unroll 4
+    for (int q = tid; q < R * 4; q += blockDim.x) {
+      const int r = q >> 2, c4 = (q & 3) * 4;
+      const float4 v = *reinterpret_cast<const float4*>(Ab + (size_t)(k0 + r) * N + k0 + c4);
+      P[r * kPS + c4] = v.x; P[r * kPS + c4 + 1] = v.y; P[r * kPS + c4 + 2] = v.z; P[r * kPS + c4 + 3] = v.w;
+    }
+  } else {
+    for (int idx = tid; idx < R * nb; idx += blockDim.x) {
+      const int r = idx / nb, c = idx % nb;
+      P[r * kPS + c] = Ab[(size_t)(k0 + r) * N + k0 + c];
+    }
   }
   __syncthreads();
 
@@ -89,34 +100,78 @@ __global__ __launch_bounds__(kLuThreads) void lu_panel_kernel(int N, int k0, flo
   }
 
   // write the factored panel back
-  for (int idx = tid; idx < R * nb; idx += blockDim.x) {
-    const int r = idx / nb, c = idx % nb;
-    Ab[(size_t)(k0 + r) * N + k0 + c] = P[r * kPS + c];
+  if (vec) {
+#pragma unroll 4
+    for (int q = tid; q < R * 4; q += blockDim.x) {
+      const int r = q >> 2, c4 = (q & 3) * 4;
+      *reinterpret_cast<float4*>(Ab + (size_t)(k0 + r) * N + k0 + c4) =
+          make_float4(P[r * kPS + c4], P[r * kPS + c4 + 1], P[r * kPS + c4 + 2], P[r * kPS + c4 + 3]);
+    }
+  } else {
+    for (int idx = tid; idx < R * nb; idx += blockDim.x) {
+      const int r = idx / nb, c = idx % nb;
+      Ab[(size_t)(k0 + r) * N + k0 + c] = P[r * kPS + c];
+    }
   }
-  // row interchanges on the columns outside the panel, in pivot order (?laswp)
-  for (int j = 0; j < nb; ++j) {
-    const int p = piv[b * N + k0 + j];
-    const int rj = k0 + j;
-    if (p != rj) {
-      for (int c = tid; c < N; c += blockDim.x) {
-        if (c >= k0 && c < k0 + nb) continue;
-        const float t = Ab[(size_t)rj * N + c];
-        Ab[(size_t)rj * N + c] = Ab[(size_t)p * N + c];
-        Ab[(size_t)p * N + c] = t;
+  // Row interchanges on the columns outside the panel, in pivot order (?laswp), then
+  // U12 = L11^-1 A12 (unit lower forward substitution).  Thread t owns columns t + 256 u: it
+  // applies all interchanges to them in order (no barrier between interchanges) with the loads
+  // of kSwapCols columns in flight together; the TRSM then solves two columns at a time with
+  // their 16 loads issued before the substitution (one memory latency per step instead of one
+  // per element: this phase was latency-bound).
+  constexpr int kSwapCols = 8;
+  int pv[kNB];
+#pragma unroll
+  for (int j = 0; j < kNB; ++j) pv[j] = j < nb ? piv[b * N + k0 + j] : k0 + j;
+  for (int cb = 0; cb < N; cb += kSwapCols * kLuThreads) {
+#pragma unroll
+    for (int j = 0; j < kNB; ++j) {
+      const int rj = k0 + j, p = pv[j];
+      if (j >= nb || p == rj) continue;
+      float t0[kSwapCols], t1[kSwapCols];
+#pragma unroll
+      for (int u = 0; u < kSwapCols; ++u) {
+        const int c = cb + tid + kLuThreads * u;
+        const bool ok = c < N && (c < k0 || c >= k0 + nb);
+        t0[u] = ok ? Ab[(size_t)rj * N + c] : 0.f;
+        t1[u] = ok ? Ab[(size_t)p * N + c] : 0.f;
+      }
+#pragma unroll
+      for (int u = 0; u < kSwapCols; ++u) {
+        const int c = cb + tid + kLuThreads * u;
+        if (c < N && (c < k0 || c >= k0 + nb)) {
+          Ab[(size_t)rj * N + c] = t1[u];
+          Ab[(size_t)p * N + c] = t0[u];
+        }
       }
     }
-    __syncthreads();
   }
-  // U12 = L11^-1 A12 (unit lower, forward substitution per column)
-  for (int c = k0 + nb + tid; c < N; c += blockDim.x) {
-    float x[kNB];
+  __syncthreads();  // the TRSM's column owners differ from the interchanges' (c - k0 - nb vs c)
+  for (int c = k0 + nb + tid; c < N; c += 2 * kLuThreads) {
+    const int c2 = c + kLuThreads;
+    const bool ok2 = c2 < N;
+    float x[kNB], x2[kNB];
+#pragma unroll
+    for (int i = 0; i < kNB; ++i) {
+      x[i] = i < nb ? Ab[(size_t)(k0 + i) * N + c] : 0.f;
+      x2[i] = (i < nb && ok2) ? Ab[(size_t)(k0 + i) * N + c2] : 0.f;
+    }
+#pragma unroll
+    for (int i = 0; i < kNB; ++i) {
+      float s = x[i], s2 = x2[i];
+      for (int l = 0; l < i; ++l) {
+        const float lv = P[i * kPS + l];
+        s = s - lv * x[l];
+        s2 = s2 - lv * x2[l];
+      }
+      x[i] = s;
+      x2[i] = s2;
+    }
 #pragma unroll
     for (int i = 0; i < kNB; ++i) {
       if (i < nb) {
-        float s = Ab[(size_t)(k0 + i) * N + c];
-        for (int l = 0; l < i; ++l) s = s - P[i * kPS + l] * x[l];
-        x[i] = s;
-        Ab[(size_t)(k0 + i) * N + c] = s;
+        Ab[(size_t)(k0 + i) * N + c] = x[i];
+        if (ok2) Ab[(size_t)(k0 + i) * N + c2] = x2[i];
       }
     }
   }
@@ -145,6 +200,8 @@ __global__ __launch_bounds__(256) void lu_update_kernel(int N, int k0, float* A)
       float4 u[kNB];
 #pragma unroll
       for (int l = 0; l < kNB; ++l) u[l] = *reinterpret_cast<const float4*>(Ab + (size_t)(k0 + l) * N + c);
+      // (HBM-bound on the read + write of A22: software-pipelining the rows or batching four
+      // measured no gain, bench_stage2.py; a wider panel is what would halve the traffic)
       for (int r = 0; r < rows; ++r) {
         float4* ap = reinterpret_cast<float4*>(Ab + (size_t)(r0 + r) * N + c);
         float4 a = *ap;
@@ -174,6 +231,8 @@ __global__ __launch_bounds__(256) void lu_update_kernel(int N, int k0, float* A)
 
 // Solve (P^T L U) x = b in place for one instance per workgroup.
 constexpr int kDS = kSolveBlk + 1;  // LDS stride of the staged diagonal block
+// VEC (N % 4 == 0, 16-B aligned factors): block bounds are multiples of 4, rows 16-B aligned.
+template <bool VEC>
 __global__ __launch_bounds__(kLuThreads) void lu_solve_kernel(int N, const float* LU, const int* piv,
                                                               float* X) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
@@ -205,9 +264,29 @@ __global__ __launch_bounds__(kLuThreads) void lu_solve_kernel(int N, const float
       }
       for (int i = wave; i < nbk; i += nw) {  // prefix (forward) / suffix (backward) dot products
         const float* row = M + (size_t)(k0 + i) * N;
+        const int j0 = pass == 0 ? 0 : k1, j1 = pass == 0 ? k0 : N;
         float d = 0.f;
-        if (pass == 0) { for (int j = lane; j < k0; j += 64) d = fmaf(row[j], x[j], d); }
-        else { for (int j = k1 + lane; j < N; j += 64) d = fmaf(row[j], x[j], d); }
+        if constexpr (VEC) {
+          // 16-B loads, 4 in flight per lane: a latency-bound scalar stream ran at ~2 TB/s
+          const float4* r4 = reinterpret_cast<const float4*>(row);
+          const float4* x4 = reinterpret_cast<const float4*>(x);
+          const int q1 = j1 >> 2;
+          int q = (j0 >> 2) + lane;
+          for (; q + 192 < q1; q += 256) {
+            const float4 a0 = r4[q], a1 = r4[q + 64], a2 = r4[q + 128], a3 = r4[q + 192];
+            const float4 b0 = x4[q], b1 = x4[q + 64], b2 = x4[q + 128], b3 = x4[q + 192];
+            d = fmaf(a0.x, b0.x, d); d = fmaf(a0.y, b0.y, d); d = fmaf(a0.z, b0.z, d); d = fmaf(a0.w, b0.w, d);
+            d = fmaf(a1.x, b1.x, d); d = fmaf(a1.y, b1.y, d); d = fmaf(a1.z, b1.z, d); d = fmaf(a1.w, b1.w, d);
+            d = fmaf(a2.x, b2.x, d); d = fmaf(a2.y, b2.y, d); d = fmaf(a2.z, b2.z, d); d = fmaf(a2.w, b2.w, d);
+            d = fmaf(a3.x, b3.x, d); d = fmaf(a3.y, b3.y, d); d = fmaf(a3.z, b3.z, d); d = fmaf(a3.w, b3.w, d);
+          }
+          for (; q < q1; q += 64) {
+            const float4 a0 = r4[q], b0 = x4[q];
+            d = fmaf(a0.x, b0.x, d); d = fmaf(a0.y, b0.y, d); d = fmaf(a0.z, b0.z, d); d = fmaf(a0.w, b0.w, d);
+          }
+        } else {
+          for (int j = j0 + lane; j < j1; j += 64) d = fmaf(row[j], x[j], d);
+        }
         d = wave_sum(d);
         if (lane == 0) s[i] = d;
       }
@@ -285,8 +364,12 @@ extern "C" int iadmm_lu_solve(int64_t B, int64_t N, const float* LU, const int* 
   if (B <= 0 || N <= 0 || !LU || !piv || !x) return IADMM_E_ARG;
   const size_t lds = ((size_t)N + kSolveBlk + kSolveBlk * kDS) * sizeof(float);
   if (lds > 64 * 1024 || B > 0x7fffffff) return IADMM_E_SIZE;
-  hipLaunchKernelGGL(lu_solve_kernel, dim3((unsigned)B), dim3(kLuThreads), lds, (hipStream_t)stream,
-                     (int)N, LU, piv, x);
+  if (N % 4 == 0 && aligned16(LU))
+    hipLaunchKernelGGL(lu_solve_kernel<true>, dim3((unsigned)B), dim3(kLuThreads), lds, (hipStream_t)stream,
+                       (int)N, LU, piv, x);
+  else
+    hipLaunchKernelGGL(lu_solve_kernel<false>, dim3((unsigned)B), dim3(kLuThreads), lds, (hipStream_t)stream,
+                       (int)N, LU, piv, x);
   IADMM_CHECK_LAUNCH();
   return 0;
 }
