@@ -46,6 +46,9 @@ def parse():
     ap.add_argument("--outer_T", type=int, default=100)
     ap.add_argument("--sigma", type=float, default=6e-6)
     ap.add_argument("--cpu-sample", type=int, default=8, help="instances in the CPU baseline (0: skip)")
+    ap.add_argument("--alt-f16x3", type=int, default=1,
+                    help="also time one step of the optional split-precision cell (reported under "
+                         "'alt_precision', never as the headline value)")
     ap.add_argument("--in-place-scaling", action="store_true",
                     help="scale Q/A0 in place (no unscaled copy; residuals via the scaling identity)")
     a = ap.parse_args()
@@ -126,14 +129,14 @@ def main():
     elif not keep:
         master = None
 
-    def step(timer):
+    def step(timer, precision="f32"):
         if not keep and master is not None:
             for k in d:
                 d[k].copy_(master[k])
             torch.cuda.synchronize()
         with torch.no_grad():
             return solver.solve(params, d["Q"], d["p"], d["A0"], d["zl"], d["zu"], mi, me, T, args.sigma,
-                                keep_unscaled=keep, packed=packed, timer=timer)
+                                keep_unscaled=keep, packed=packed, timer=timer, precision=precision)
 
     for _ in range(args.warmup):
         step(None)
@@ -163,6 +166,31 @@ def main():
     kkt_bytes = B * (2.0 * (n * n + (mi + me) * n) * 4 + 10.0 * N * 4)
     cell_tf = cell_flop / (ms_cell * 1e-3) / 1e12
     kkt_gbs = kkt_bytes / (ms_kkt * 1e-3) / 1e9
+
+    # optional split-precision mode: one step after the headline steps, reported beside it
+    alt = None
+    if args.alt_f16x3 and h % 8 == 0 and (keep or master is not None):
+        x32 = out["x"].clone()
+        for k in ("H", "C"):
+            out.pop(k, None)
+        timer16 = solver.Timer(True)
+        if dist:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        out16 = step(timer16, "f16x3")
+        torch.cuda.synchronize()
+        el16 = parallel.max_over_ranks(time.perf_counter() - t0, dist, device="cuda")
+        n16, ms16 = timer16.stats_ms("k:lstm_cell")
+        alt = {"mode": "f16x3",
+               "note": "optional split-precision gate GEMM (3-term fp16 split, fp32 accumulation, "
+                       "csrc/lstm_f16x3.hip); not the headline value",
+               "value": world * B / el16, "unit": "QP instances/s", "ms_per_step": 1e3 * el16,
+               "cell_avg_launch_ms": ms16, "cell_tflops_f32_equiv": cell_flop / (ms16 * 1e-3) / 1e12,
+               "final_residual": {"primal_mean": float(out16["primal"].mean()),
+                                  "dual_mean": float(out16["dual"].mean())},
+               "x_rel_l2_vs_f32_run": float((out16["x"] - x32).norm() / x32.norm().clamp_min(1e-30))}
+        del out16
 
     res = None
     if rank == 0:
@@ -199,6 +227,8 @@ def main():
                                 "algorithmic_per_launch": kkt_bytes},
             "phase_ms_per_step": {k: v / args.steps for k, v in spans.items() if not k.startswith("k:")},
         }
+        if alt is not None:
+            res["alt_precision"] = alt
         if args.cpu_sample > 0 and world == 1:  # the CPU baseline is an N=1 figure
             res["cpu_baseline"] = cpu_baseline(args, d if keep else master, params)
         print(json.dumps(res), flush=True)

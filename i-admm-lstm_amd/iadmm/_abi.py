@@ -25,6 +25,10 @@ SIGNATURES = {
     "iadmm_lstm_ntiles": (i64, [i64]),
     "iadmm_lstm_pack": (cint, [i64] + [vp] * 13 + [vp, vp, vp]),
     "iadmm_lstm_cell_fwd": (cint, [i64, i64, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp]),
+    "iadmm_lstm_packed16_halfs": (i64, [i64]),
+    "iadmm_lstm_pack_f16x3": (cint, [i64, vp, vp, vp, vp, vp, vp, vp]),
+    "iadmm_split_f16": (cint, [i64, vp, vp, vp]),
+    "iadmm_lstm_cell_fwd_f16x3": (cint, [i64, i64, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp]),
     "iadmm_admm_update": (cint, [i64, i64, i64, i64, i64, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, cint,
                                  vp, vp, vp, vp, vp, vp]),
     "iadmm_ruiz_scale": (cint, [i64, i64, i64, i64, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp]),

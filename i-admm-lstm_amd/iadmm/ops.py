@@ -104,6 +104,46 @@ def lstm_cell(H, C, xv, g, Upk, Wx, Hn=None, Cn=None, part=None):
     return Hn, Cn, part
 
 
+# --------------------------------------------------------------------------- optional f16x3 cell
+def _p16(t):
+    """Device pointer of a contiguous fp16 device tensor (the split planes of csrc/lstm_f16x3.hip)."""
+    if t is None:
+        return None
+    if not t.is_cuda or t.dtype != torch.float16 or not t.is_contiguous():
+        raise TypeError("split planes must be contiguous float16 device tensors")
+    return t.data_ptr()
+
+
+def lstm_pack_f16x3(params, h):
+    """Split, power-of-two-scaled gate weights (Upk16 [2 planes], wscale [2])."""
+    L = _abi.lib()
+    ref = params["U_i"]
+    Upk16 = torch.empty(int(L.iadmm_lstm_packed16_halfs(h)), dtype=torch.float16, device=ref.device)
+    wscale = empty(2, like=ref)
+    us = [_c(params[k]) for k in ("U_i", "U_f", "U_o", "U_u")]
+    _abi.call("iadmm_lstm_pack_f16x3", int(h), *[_p(t) for t in us], _p16(Upk16), _p(wscale), _stream())
+    return Upk16, wscale
+
+
+def split_f16(X, out=None):
+    """[2, *X.shape] fp16 planes (hi, lo) of an fp32 tensor."""
+    out = torch.empty((2,) + tuple(X.shape), dtype=torch.float16, device=X.device) if out is None else out
+    _abi.call("iadmm_split_f16", X.numel(), _p(X), _p16(out), _stream())
+    return out
+
+
+def lstm_cell_f16x3(H16, C, xv, g, Upk16, wscale, Wx, Hn16=None, Cn=None, part=None, Hn=None):
+    """Split-precision cell: H16 [2, M, h] planes -> (Hn16, Cn, part, Hn); Hn (fp32) only if given."""
+    h = H16.shape[-1]
+    M = H16[0].numel() // h
+    Hn16 = torch.empty_like(H16) if Hn16 is None else Hn16
+    Cn = torch.empty_like(C) if Cn is None else Cn
+    part = empty(lstm_ntiles(h), M, like=C) if part is None else part
+    _abi.call("iadmm_lstm_cell_fwd_f16x3", M, h, _p16(H16), _p(C), _p(xv), _p(g), _p16(Upk16), _p(Wx),
+              _p(wscale), _p(Hn), _p16(Hn16), _p(Cn), _p(part), _stream())
+    return Hn16, Cn, part, Hn
+
+
 # --------------------------------------------------------------------------- ADMM update
 def admm_update(n, m, num_ineq, part, b_h, xv, x, y, z, zl, zu, scal, relax_z=False, out=None,
                 rho_vec=None, rho_rows=None):

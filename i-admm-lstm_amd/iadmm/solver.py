@@ -32,16 +32,30 @@ class PackedWeights:
     ``_version``; replacing a tensor changes its data_ptr)."""
 
     def __init__(self):
-        self._key = None
-        self.Upk = self.Wx = None
+        self._key = self._key16 = None
+        self.Upk = self.Wx = self.Upk16 = self.wscale = None
+
+    @staticmethod
+    def _version_key(params, h):
+        return tuple((params[k].data_ptr(), params[k]._version) for k in PARAM_NAMES[:13]) + (h,)
 
     def get(self, params, h):
-        key = tuple((params[k].data_ptr(), params[k]._version) for k in PARAM_NAMES[:13]) + (h,)
+        key = self._version_key(params, h)
         if key != self._key:
             with torch.no_grad():
                 self.Upk, self.Wx = ops.lstm_pack(params, h)
             self._key = key
         return self.Upk, self.Wx
+
+    def get_f16x3(self, params, h):
+        """Split weights of the optional f16x3 cell: (Upk16, wscale, Wx)."""
+        _, Wx = self.get(params, h)
+        key = self._version_key(params, h)
+        if key != self._key16:
+            with torch.no_grad():
+                self.Upk16, self.wscale = ops.lstm_pack_f16x3(params, h)
+            self._key16 = key
+        return self.Upk16, self.wscale, Wx
 
 
 class Timer:
@@ -81,8 +95,11 @@ class Timer:
         self.spans = {}
 
 
+PRECISIONS = ("f32", "f16x3")
+
+
 def solve(params, Q, p, A0, zl, zu, num_ineq, num_eq, T, sigma, scaling=True, scaling_iters=10,
-          keep_unscaled=True, history=False, packed=None, timer=None, iter_hook=None):
+          keep_unscaled=True, history=False, packed=None, timer=None, iter_hook=None, precision="f32"):
     """Solve one batch; returns a dict with unscaled x/y/z, scaled state, final residuals.
 
     Q[B,n,n], p[B,n,1], A0[B,m,n], zl/zu[B,m,1] fp32 device tensors (unscaled, Q already *2 as
@@ -90,7 +107,13 @@ def solve(params, Q, p, A0, zl, zu, num_ineq, num_eq, T, sigma, scaling=True, sc
     bench config) and reports residuals through the scaling identity instead of the originals.
     ``history=True`` records per-iteration obj / ls_res / primal / dual on the device and calls
     ``iter_hook(t, x, y, z)`` with the unscaled iterate ([B,n], [B,m], [B,m]) after each step.
+    ``precision="f16x3"`` runs the gate GEMM on the fp16 matrix cores with the 3-term split of
+    csrc/lstm_f16x3.hip (optional mode; the default "f32" is the fp32-MFMA path): H is carried as
+    its two fp16 planes between iterations and the fp32 H is written on the last iteration.
     """
+    if precision not in PRECISIONS:
+        raise ValueError(f"precision must be one of {PRECISIONS}")
+    f16 = precision == "f16x3"
     params = param_dict(params)
     B, n = Q.shape[0], Q.shape[1]
     m = A0.shape[1]
@@ -103,7 +126,10 @@ def solve(params, Q, p, A0, zl, zu, num_ineq, num_eq, T, sigma, scaling=True, sc
     N = n + m
     timer = timer or Timer(False)
     packed = packed or PackedWeights()
-    Upk, Wx = packed.get(params, h)
+    if f16:
+        Upk16, wscale, Wx = packed.get_f16x3(params, h)
+    else:
+        Upk, Wx = packed.get(params, h)
     rho_p, alpha_p, b_h = (params[k].detach().contiguous() for k in ("rho", "alpha", "b_h"))
 
     f32 = dict(dtype=torch.float32, device=dev)
@@ -121,7 +147,12 @@ def solve(params, Q, p, A0, zl, zu, num_ineq, num_eq, T, sigma, scaling=True, sc
     ys = [torch.zeros(B, m, **f32), torch.empty(B, m, **f32)]
     zs = [torch.zeros(B, m, **f32), torch.empty(B, m, **f32)]
     xvs = [torch.zeros(B, N, **f32), torch.empty(B, N, **f32)]
-    Hs = [torch.zeros(B, N, h, **f32), torch.empty(B, N, h, **f32)]
+    if f16:  # split planes of H (ping-pong) + the fp32 H written on the last iteration
+        f16t = dict(dtype=torch.float16, device=dev)
+        H16s = [torch.zeros(2, B, N, h, **f16t), torch.empty(2, B, N, h, **f16t)]
+        Hs = [torch.zeros(B, N, h, **f32)] * 2
+    else:
+        Hs = [torch.zeros(B, N, h, **f32), torch.empty(B, N, h, **f32)]
     C = torch.zeros(B, N, h, **f32)
     g = torch.empty(B, N, **f32)
     part = torch.empty(ops.lstm_ntiles(h), B * N, **f32)
@@ -140,7 +171,11 @@ def solve(params, Q, p, A0, zl, zu, num_ineq, num_eq, T, sigma, scaling=True, sc
         ops.kkt_resgrad(Qs, As, pv, xs[cur], ys[cur], zs[cur], xvs[cur], sigma, scal, num_ineq, g=g)
         timer.stop(k)
         k = timer.start("k:lstm_cell")
-        ops.lstm_cell(Hs[cur], C, xvs[cur], g, Upk, Wx, Hn=Hs[nxt], Cn=C, part=part)
+        if f16:
+            ops.lstm_cell_f16x3(H16s[cur], C, xvs[cur], g, Upk16, wscale, Wx, Hn16=H16s[nxt], Cn=C, part=part,
+                                Hn=Hs[0] if t == T - 1 else None)
+        else:
+            ops.lstm_cell(Hs[cur], C, xvs[cur], g, Upk, Wx, Hn=Hs[nxt], Cn=C, part=part)
         timer.stop(k)
         ops.admm_update(n, m, num_ineq, part, b_h, xvs[cur], xs[cur], ys[cur], zs[cur], zlv, zuv, scal,
                         out=(xvs[nxt], xs[nxt], ys[nxt], zs[nxt]))
@@ -171,7 +206,7 @@ def solve(params, Q, p, A0, zl, zu, num_ineq, num_eq, T, sigma, scaling=True, sc
     obj, pr, du = _metrics(Q, p, A0, Qs, ps, As, D, E, c, x, y, z, xs[cur], ys[cur], zs[cur],
                            keep_unscaled or not scaling)
     out = dict(x=x.unsqueeze(-1), y=y.unsqueeze(-1), z=z.unsqueeze(-1), xv=xvs[cur].unsqueeze(-1),
-               H=Hs[cur], C=C, x_scaled=xs[cur].unsqueeze(-1), y_scaled=ys[cur].unsqueeze(-1),
+               H=Hs[0] if f16 else Hs[cur], C=C, x_scaled=xs[cur].unsqueeze(-1), y_scaled=ys[cur].unsqueeze(-1),
                z_scaled=zs[cur].unsqueeze(-1), obj=obj, primal=pr, dual=du, scal=scal,
                scaled=(Qs, ps, As, zls, zus), D=D, E=E, c=c)
     if history:

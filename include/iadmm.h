@@ -132,6 +132,29 @@ int iadmm_lstm_cell_fwd(int64_t M, int64_t h, const float* H, const float* C,
                         const float* xv, const float* g, const float* Upk, const float* Wx,
                         float* Hn, float* Cn, float* part, void* stream);
 
+/* ---- Optional split-precision cell ("f16x3"; not the default path) ----------------------------
+ * The same cell with the hidden x gate contraction on the fp16 matrix cores
+ * (v_mfma_f32_32x32x16_f16) using a 3-term split x = hi + lo of both operands
+ * (U.H ~= U_hi H_hi + U_hi H_lo + U_lo H_hi, fp32 accumulation; error analysis in
+ * csrc/lstm_f16x3.hip).  Half buffers are passed as void* (IEEE binary16). */
+
+/* Halfs of the split weight layout for hidden size h (2 planes of the iadmm_lstm_pack layout). */
+int64_t iadmm_lstm_packed16_halfs(int64_t h);
+
+/* Split, power-of-two-scaled U_{i,f,o,u}[h,h] -> Upk16; wscale[2] = {2^s, 2^-s} (device). */
+int iadmm_lstm_pack_f16x3(int64_t h, const float* U_i, const float* U_f, const float* U_o,
+                          const float* U_u, void* Upk16, float* wscale, void* stream);
+
+/* Y16[0..n) = fp16(x), Y16[n..2n) = fp16(x - fp16(x)) (the split planes of an fp32 tensor). */
+int iadmm_split_f16(int64_t n, const float* X, void* Y16, void* stream);
+
+/* Cell with split H: H16[2][M][h] -> Hn16[2][M][h] (must not alias H16), Cn[M,h] (may alias C),
+ * part[ntiles][M]; the fp32 H' is written to Hn only when Hn != NULL.  Requires h % 8 == 0 and
+ * 16-B aligned H16, Hn16, Upk16, C, Cn, Hn.  Wx from iadmm_lstm_pack. */
+int iadmm_lstm_cell_fwd_f16x3(int64_t M, int64_t h, const void* H16, const float* C, const float* xv,
+                              const float* g, const void* Upk16, const float* Wx, const float* wscale,
+                              float* Hn, void* Hn16, float* Cn, float* part, void* stream);
+
 /* ADMM update (replaces models/lstm.py:80 ``+ b_h`` and :82-94):
  * grad = sum_tiles part + b_h ; xv' = xv - grad ; x' = alpha xv'[:n] + (1-alpha) x ;
  * z~ = z + (v - y)/rho ; z' = clamp(z~ + y/rho, zl, zu) ; y' = y + rho (z~ - z').
