@@ -33,7 +33,7 @@ IADMM_DEV void cell_tile_of_block(int njt, int& jt, int& rt) {
 // acc[g][r] (4 gates x 2 row blocks of 32x32) = U_g[:, jt*32 .. +32]^T . H[rbase + wave*64 + r*32 ..]^T
 // NW waves per workgroup (64*NW data rows).  PRIO: 0 none; 1 s_setprio(1) around each MFMA
 // cluster; 2 (NW = 8) static priority 1 for waves 4-7 (cdna_hip_programming.md T5).
-template <bool VEC, int NW = 4, int PRIO = 0>
+template <bool VEC, int NW = 4, int PRIO = 0, bool BUF = false>
 IADMM_DEV void cell_mainloop(const float* __restrict__ H, int64_t M, int h, int nkc,
                              const float* __restrict__ Ubase, int64_t rbase, float* sA, float* sB,
                              floatx16 (&acc)[4][2], int tid, int wave, int jl, int hf) {
@@ -53,11 +53,23 @@ IADMM_DEV void cell_mainloop(const float* __restrict__ H, int64_t M, int h, int 
   // Staging registers as named scalars (an array here was turned into an LDS/scratch alloca
   // by the compiler, which then waited for each global load right after issuing it).
   float4 ra0, ra1, ra2, ra3, rb0, rb1, rb2, rb3, rb4, rb5, rb6, rb7;
+  // BUF: the H panel through a buffer descriptor whose range ends at the last valid row, so a
+  // row past M (and a k past h, offset forced out of range) reads 0 without a branch: no
+  // predicated load, no phi, no early vmcnt wait.
+  const int64_t nvalid = (M - rbase) < NT ? (M - rbase) : NT;
+  const __amdgpu_buffer_rsrc_t hrs = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float*>(H + rbase * h), 0, (int)(nvalid * h * 4), 0x00020000);
   auto ldB = [&](int kc, int i) -> float4 {
     const int idx = tid + NT * i, row = idx >> 3, c4 = idx & 7;
     const int64_t R = rbase + row;
     const int k = kc * kBK + c4 * 4;
-    if constexpr (VEC) {
+    if constexpr (BUF) {
+      static_assert(VEC, "BUF needs h % 4 == 0");
+      const unsigned off = k < h ? (unsigned)(row * h + k) * 4u : 0x80000000u;
+      typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+      const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(hrs, off, 0, 0);
+      return make_float4(__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z), __uint_as_float(v.w));
+    } else if constexpr (VEC) {
       return (R < M && k < h) ? *reinterpret_cast<const float4*>(H + R * h + k) : make_float4(0.f, 0.f, 0.f, 0.f);
     } else {
       float4 t;
@@ -115,73 +127,233 @@ IADMM_DEV void cell_mainloop(const float* __restrict__ H, int64_t M, int h, int 
   if constexpr (PRIO == 2) __builtin_amdgcn_s_setprio(0);
 }
 
-// The forward cell kernel (production instance: NW = 4, PRIO = 0, lstm.hip): fp32-MFMA gate GEMM
-// (cell_mainloop) + the fused cell epilogue.  Workgroup = 32 hidden units x 64*NW rows.
-template <bool VEC, int NW = 4, int PRIO = 0>
-__global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void cell_fwd_kernel(CellArgsT a) {
-  constexpr int ROWS = 64 * NW;
-  __shared__ __attribute__((aligned(16))) float sA[128 * kLD];
-  __shared__ __attribute__((aligned(16))) float sB[ROWS * kLD];
-  __shared__ __attribute__((aligned(16))) float sW[kWxF * kJT];
 
-  int jt, rt;
-  cell_tile_of_block(a.njt, jt, rt);
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int jl = lane & 31, hf = lane >> 5;
+// ---- LDS-DMA main loop (gfx950 buffer_load_dwordx4 ... lds): same products, same accumulation
+// order as cell_mainloop (k = 32*kc32 + 8*G + 4*hf + s), so the result is bitwise identical.
+//
+// K is staged in 16-deep chunks through a 3-stage LDS ring filled directly by LDS-DMA (no staging
+// registers, no ds_write pass): per chunk and wave, 2 pieces of the weight tile + 4 pieces of the
+// H panel (1 KiB each).  Every LDS row is 16 floats (64 B) with its four 16-B slots XOR-swizzled
+// by (row >> 2) & 3 on the SOURCE address (the DMA image is lane-linear), which makes the
+// fragment ds_read_b128 conflict-free.  One barrier per chunk, placed between the two 8-deep
+// halves: before it, each wave waits only for its own pieces of chunk kc+1 (counted vmcnt, chunk
+// kc+2 never in flight yet); after it, chunk kc+2 is issued into the stage chunk kc-1 used and the
+// first fragments of chunk kc+1 are read while the second half of chunk kc runs on the MFMA pipe.
+// Fragments are double-buffered in registers so no MFMA waits on an LDS read it just issued.
+constexpr int kBKd = 16;                          // K chunk of the DMA ring
+constexpr int kStages = 3;
+constexpr int kStageA = 128 * kBKd;               // floats: 4 gates x 32 units x 16 k
+constexpr int kStageB = 256 * kBKd;               // floats: 256 rows x 16 k
+constexpr int kRingFloats = kStages * (kStageA + kStageB);  // 73728 B
+
+typedef __attribute__((address_space(3))) void lds_void;
+
+template <int N>
+IADMM_DEV void vm_wait() {  // s_waitcnt vmcnt(N), other counters untouched (gfx9 encoding)
+  __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
+}
+
+// acc[g][r] as cell_mainloop; Ubase = Upk + jt*nkc32*128*32 (fp32 32-deep packing), ring = LDS.
+// before_last() runs once, just before the last chunk's MFMAs (e.g. to prefetch epilogue operands
+// behind them).
+template <class BeforeLast>
+IADMM_DEV void cell_mainloop_dma(const float* __restrict__ H, int64_t M, int h, int nkc32,
+                                 const float* __restrict__ Ubase, int64_t rbase, float* ring,
+                                 floatx16 (&acc)[4][2], int tid, int wave, int jl, int hf,
+                                 BeforeLast&& before_last) {
+#pragma unroll
+  for (int g = 0; g < 4; ++g)
+#pragma unroll
+    for (int r = 0; r < 2; ++r)
+#pragma unroll
+      for (int q = 0; q < 16; ++q) acc[g][r][q] = 0.f;
+
+  const int lane = tid & 63;
+  const int nk = (h + kBKd - 1) / kBKd;
+  const int64_t nvalid = (M - rbase) < 256 ? (M - rbase) : 256;
+  const __amdgpu_buffer_rsrc_t hrs = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float*>(H + rbase * h), 0, (int)(nvalid * h * 4), 0x00020000);
+  const __amdgpu_buffer_rsrc_t urs = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float*>(Ubase), 0, nkc32 * 128 * kBK * 4, 0x00020000);
+
+  // Per-lane source offsets of this wave's pieces (piece = 16 LDS rows x 4 slots).
+  const int prow = lane >> 2, pslot = lane & 3;
+  unsigned aoff[2];
+  int bk4[4];
+  unsigned boff[4];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int row = (wave * 2 + i) * 16 + prow;             // g*32 + jj
+    const int c = pslot ^ ((row >> 2) & 3);
+    aoff[i] = (unsigned)(row * kBK + c * 4) * 4u;            // + kc32*16 KiB + half*64 B
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int row = (wave * 4 + i) * 16 + prow;
+    const int c = pslot ^ ((row >> 2) & 3);
+    bk4[i] = c * 4;
+    boff[i] = (unsigned)(row * h + c * 4) * 4u;              // + kc*64 B
+  }
+  auto issue = [&](int kc) {
+    const int st = kc % kStages;
+    float* sa = ring + st * (kStageA + kStageB);
+    float* sb = sa + kStageA;
+    const unsigned ua = (unsigned)((kc >> 1) * 128 * kBK + (kc & 1) * kBKd) * 4u;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(urs, (lds_void*)(sa + (wave * 2 + i) * 256), 16,
+                                               aoff[i] + ua, 0, 0, 0);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const unsigned o = (kc * kBKd + bk4[i] < h) ? boff[i] + (unsigned)(kc * kBKd * 4) : 0x80000000u;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(hrs, (lds_void*)(sb + (wave * 4 + i) * 256), 16, o, 0, 0, 0);
+    }
+  };
+  // Fragment addresses: row (g*32 + jl) / (wave*64 + r*32 + jl), slot (2G + hf) ^ ((jl >> 2) & 3).
+  const int sw = (jl >> 2) & 3;
+  const int aoffG[2] = {jl * kBKd + 4 * ((0 + hf) ^ sw), jl * kBKd + 4 * ((2 + hf) ^ sw)};
+  const int boffG[2] = {(wave * 64 + jl) * kBKd + 4 * ((0 + hf) ^ sw),
+                        (wave * 64 + jl) * kBKd + 4 * ((2 + hf) ^ sw)};
+  float4 fa0[4], fb0[2], fa1[4], fb1[2];
+  auto frag = [&](int kc, int G, float4 (&fa)[4], float4 (&fb)[2]) {
+    const float* sa = ring + (kc % kStages) * (kStageA + kStageB);
+    const float* sb = sa + kStageA;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) fa[g] = *reinterpret_cast<const float4*>(sa + g * 32 * kBKd + aoffG[G]);
+#pragma unroll
+    for (int r = 0; r < 2; ++r) fb[r] = *reinterpret_cast<const float4*>(sb + r * 32 * kBKd + boffG[G]);
+  };
+  auto mma = [&](const float4 (&fa)[4], const float4 (&fb)[2]) {
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+#pragma unroll
+        for (int r = 0; r < 2; ++r)
+          acc[g][r] = __builtin_amdgcn_mfma_f32_32x32x2f32(get4(fa[g], s), get4(fb[r], s), acc[g][r], 0, 0, 0);
+  };
+
+  issue(0);
+  if (nk > 1) issue(1);
+  if (nk > 1) vm_wait<6>(); else vm_wait<0>();
+  __builtin_amdgcn_s_barrier();
+  frag(0, 0, fa0, fb0);
+  // The schedule is pinned with sched_group_barrier (the compiler otherwise sinks every fragment
+  // read to just before the MFMA that consumes it and bunches the DMA issues): each LDS read and
+  // each LDS-DMA piece gets an MFMA of its own to hide behind.  The DMA of chunk kc+2 is issued
+  // unconditionally (past the last chunk its offsets are out of range: no traffic, zeros into a
+  // stage nobody reads), so the loop body is one basic block.
+  for (int kc = 0; kc < nk - 1; ++kc) {
+    frag(kc, 1, fa1, fb1);
+    mma(fa0, fb0);
+#pragma unroll
+    for (int i = 0; i < 6; ++i) {
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // DS read
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
+    }
+    __builtin_amdgcn_sched_group_barrier(0x008, 26, 0);
+    __builtin_amdgcn_sched_barrier(0);
+    vm_wait<0>();  // this wave's pieces of chunk kc+1 (chunk kc+2 is not issued yet)
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    issue(kc + 2);
+    frag(kc + 1, 0, fa0, fb0);
+    mma(fa1, fb1);
+#pragma unroll
+    for (int i = 0; i < 6; ++i) {
+      __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);  // VMEM (LDS-DMA piece)
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < 6; ++i) {
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+    }
+    __builtin_amdgcn_sched_group_barrier(0x008, 20, 0);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  frag(nk - 1, 1, fa1, fb1);  // last chunk, peeled
+  before_last();
+  __builtin_amdgcn_sched_barrier(0);
+  mma(fa0, fb0);
+  mma(fa1, fb1);
+}
+
+// The fused cell epilogue: gates, C' = I U + F C, H' = O tanh(C'), projection partial, from the
+// accumulators of a 32-unit x (wave's 64 rows) tile.  sW = the tile's Wx rows ([32 units][16 fields]).
+// Split in two so a kernel can issue the global loads (cell_epi_load) early, e.g. before its last
+// K chunk, and keep them in registers until cell_epi_compute.
+// accumulator element q of lane (jl,hf): hidden jj = (q&3) + 8*(q>>2) + 4*hf, data row jl.
+struct CellEpiIn {
+  float4 cold[2][4];  // C[R, jt*32 + 8*qq + 4*hf .. +4] for the lane's two rows
+  float in0[2], in1[2];
+};
+
+template <bool VEC>
+IADMM_DEV void cell_epi_load(const CellArgsT& a, int jt, int64_t rbase, int wave, int jl, int hf, CellEpiIn& e) {
+  const int h = a.h;
+#pragma unroll
+  for (int r = 0; r < 2; ++r) {
+    const int64_t R = rbase + wave * 64 + r * 32 + jl;
+    const bool rok = R < a.M;
+    e.in0[r] = rok ? a.xv[R] : 0.f;
+    e.in1[r] = rok ? a.g[R] : 0.f;
+#pragma unroll
+    for (int qq = 0; qq < 4; ++qq) {
+      const int j0 = jt * kJT + 8 * qq + 4 * hf;
+      if constexpr (VEC) {
+        e.cold[r][qq] = (rok && j0 < h) ? *reinterpret_cast<const float4*>(a.C + R * h + j0)
+                                        : make_float4(0.f, 0.f, 0.f, 0.f);
+      } else {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) set4(e.cold[r][qq], k, (rok && j0 + k < h) ? a.C[R * h + j0 + k] : 0.f);
+      }
+    }
+  }
+}
+
+template <bool VEC>
+IADMM_DEV void cell_epi_compute(const CellArgsT& a, floatx16 (&acc)[4][2], const float* sW, int jt,
+                                int64_t rbase, int wave, int jl, int hf, const CellEpiIn& ei) {
   const int h = a.h;
   const int64_t M = a.M;
-  const int64_t rbase = (int64_t)rt * ROWS;
-
-  for (int i = tid; i < kWxF * kJT; i += 64 * NW) {
-    const int f = i / kJT, jj = i % kJT;
-    sW[i] = a.Wx[(int64_t)(jt * kJT + jj) * kWxF + f];
-  }
-
-  floatx16 acc[4][2];
-  cell_mainloop<VEC, NW, PRIO>(a.H, M, h, a.nkc32, a.Upk + (int64_t)jt * a.nkc32 * 128 * kBK, rbase, sA, sB,
-                               acc, tid, wave, jl, hf);
-
-  // ---- epilogue: gates, cell update, projection partial (all in registers)
-  // accumulator element q of lane (jl,hf): hidden jj = (q&3) + 8*(q>>2) + 4*hf, data row jl.
 #pragma unroll
   for (int r = 0; r < 2; ++r) {
     const int64_t R = rbase + wave * 64 + r * 32 + jl;
     const bool rok = R < M;
-    const float in0 = rok ? a.xv[R] : 0.f;
-    const float in1 = rok ? a.g[R] : 0.f;
+    const float in0 = ei.in0[r], in1 = ei.in1[r];
     float gsum = 0.f;
 #pragma unroll
     for (int qq = 0; qq < 4; ++qq) {
+      __builtin_amdgcn_sched_barrier(0);  // one (rows, 4 units) group at a time: bounded live range
       const int jj0 = 8 * qq + 4 * hf;
       const int j0 = jt * kJT + jj0;
-      float4 cold;
-      if constexpr (VEC) {
-        cold = (rok && j0 < h) ? *reinterpret_cast<const float4*>(a.C + R * h + j0)
-                               : make_float4(0.f, 0.f, 0.f, 0.f);
-      } else {
-#pragma unroll
-        for (int e = 0; e < 4; ++e) set4(cold, e, (rok && j0 + e < h) ? a.C[R * h + j0 + e] : 0.f);
-      }
-      float4 wv[13];
-#pragma unroll
-      for (int f = 0; f < 13; ++f) wv[f] = *reinterpret_cast<const float4*>(&sW[f * kJT + jj0]);
+      const float4 cold = ei.cold[r][qq];
       float4 cnew, hnew;
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const int q = qq * 4 + e;
+        // unit jj0+e: its 16 packed fields (Wx layout), one 64-B row of sW (same address across
+        // the 32 lanes of a half-wave: broadcast)
+        float wf[16];
+#pragma unroll
+        for (int f4 = 0; f4 < 4; ++f4) {
+          const float4 t = *reinterpret_cast<const float4*>(&sW[(jj0 + e) * kWxF + 4 * f4]);
+          wf[4 * f4] = t.x; wf[4 * f4 + 1] = t.y; wf[4 * f4 + 2] = t.z; wf[4 * f4 + 3] = t.w;
+        }
         float pre[4];
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
-          const float xw = in0 * get4(wv[3 * g], e) + in1 * get4(wv[3 * g + 1], e);
-          pre[g] = (xw + acc[g][r][q]) + get4(wv[3 * g + 2], e);
+          const float xw = in0 * wf[3 * g] + in1 * wf[3 * g + 1];
+          pre[g] = (xw + acc[g][r][q]) + wf[3 * g + 2];
         }
-        const float ig = sigmoidf_(pre[0]), fg = sigmoidf_(pre[1]), og = sigmoidf_(pre[2]);
-        const float ug = tanhf(pre[3]);
+        const float ig = sigmoid_cell(pre[0]), fg = sigmoid_cell(pre[1]), og = sigmoid_cell(pre[2]);
+        const float ug = tanh_cell(pre[3]);
         const float c2 = ig * ug + fg * get4(cold, e);
-        const float h2 = og * tanhf(c2);
+        const float h2 = og * tanh_cell(c2);
         set4(cnew, e, c2);
         set4(hnew, e, h2);
-        gsum = fmaf(h2, get4(wv[12], e), gsum);
+        gsum = fmaf(h2, wf[12], gsum);
       }
       if (rok) {
         if constexpr (VEC) {
@@ -204,5 +376,75 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void cell_fwd_kernel(Cell
     if (hf == 0 && rok) a.part[(int64_t)jt * M + R] = gsum;
   }
 }
+
+template <bool VEC>
+IADMM_DEV void cell_epilogue(const CellArgsT& a, floatx16 (&acc)[4][2], const float* sW, int jt,
+                             int64_t rbase, int wave, int jl, int hf) {
+  CellEpiIn ei;
+  cell_epi_load<VEC>(a, jt, rbase, wave, jl, hf, ei);
+  cell_epi_compute<VEC>(a, acc, sW, jt, rbase, wave, jl, hf, ei);
+}
+
+// The forward cell kernel (production instance: NW = 4, PRIO = 0, lstm.hip): fp32-MFMA gate GEMM
+// (cell_mainloop) + the fused cell epilogue.  Workgroup = 32 hidden units x 64*NW rows.
+template <bool VEC, int NW = 4, int PRIO = 0, bool BUF = false>
+__global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void cell_fwd_kernel(CellArgsT a) {
+  constexpr int ROWS = 64 * NW;
+  __shared__ __attribute__((aligned(16))) float sA[128 * kLD];
+  __shared__ __attribute__((aligned(16))) float sB[ROWS * kLD];
+  __shared__ __attribute__((aligned(16))) float sW[kWxF * kJT];
+
+  int jt, rt;
+  cell_tile_of_block(a.njt, jt, rt);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int jl = lane & 31, hf = lane >> 5;
+  const int h = a.h;
+  const int64_t M = a.M;
+  const int64_t rbase = (int64_t)rt * ROWS;
+
+  for (int i = tid; i < kWxF * kJT; i += 64 * NW) sW[i] = a.Wx[(int64_t)jt * kJT * kWxF + i];
+
+  floatx16 acc[4][2];
+  cell_mainloop<VEC, NW, PRIO, BUF>(a.H, M, h, a.nkc32, a.Upk + (int64_t)jt * a.nkc32 * 128 * kBK, rbase, sA, sB,
+                               acc, tid, wave, jl, hf);
+
+  cell_epilogue<VEC>(a, acc, sW, jt, rbase, wave, jl, hf);
+}
+
+
+// Forward cell kernel on the LDS-DMA main loop (VEC only: h % 4 == 0, 16-B aligned rows).
+// Dynamic LDS: kRingFloats + kWxF*kJT floats (74 KiB) -> 2 workgroups per CU.
+// DIAG (timing tools only): 1 = skip the epilogue (main-loop cost).
+template <int DIAG = 0>
+__global__ __launch_bounds__(256, 2) void cell_fwd_dma_kernel(CellArgsT a) {
+  extern __shared__ __attribute__((aligned(16))) float dsm[];
+  float* ring = dsm;
+  float* sW = dsm + kRingFloats;
+  int jt, rt;
+  cell_tile_of_block(a.njt, jt, rt);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int jl = lane & 31, hf = lane >> 5;
+  const int64_t rbase = (int64_t)rt * kRows;
+  for (int i = tid; i < kWxF * kJT; i += 256) sW[i] = a.Wx[(int64_t)jt * kJT * kWxF + i];
+  floatx16 acc[4][2];
+  CellEpiIn ei;
+  cell_mainloop_dma(a.H, a.M, a.h, a.nkc32, a.Upk + (int64_t)jt * a.nkc32 * 128 * kBK, rbase, ring, acc,
+                    tid, wave, jl, hf, [&] { cell_epi_load<true>(a, jt, rbase, wave, jl, hf, ei); });
+  if constexpr (DIAG == 1) {
+    float t = 0.f;
+#pragma unroll
+    for (int g = 0; g < 4; ++g)
+#pragma unroll
+      for (int r = 0; r < 2; ++r)
+#pragma unroll
+        for (int q = 0; q < 16; ++q) t += acc[g][r][q];
+    a.part[(int64_t)blockIdx.x * 256 + tid] = t;
+    return;
+  }
+  __syncthreads();  // sW visible (written before the main loop)
+  cell_epi_compute<true>(a, acc, sW, jt, rbase, wave, jl, hf, ei);
+}
+constexpr int kDmaLdsBytes = (kRingFloats + kWxF * kJT) * 4;
 
 }  // namespace iadmm

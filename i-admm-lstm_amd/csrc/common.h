@@ -32,6 +32,24 @@ IADMM_DEV float tmax(float a, float b) { return (a != a || b != b) ? __builtin_n
 
 IADMM_DEV float sigmoidf_(float x) { return 1.0f / (1.0f + expf(-x)); }
 
+// LSTM-cell transcendentals (branch-free, <= 2 ulp; tools/mathcheck.hip measures them against
+// fp64 over the fp32 range the gates see).  sigmoid: accurate expf, hardware reciprocal in place of
+// the IEEE division.  tanh: odd minimax polynomial x + x^3 P(x^2) on |x| < 0.625 (approximation
+// error 4.5e-9 relative), 1 - 2/(e^{2|x|} + 1) above (no cancellation there: 2/(e+1) <= 0.45).
+IADMM_DEV float sigmoid_cell(float x) { return __builtin_amdgcn_rcpf(1.0f + expf(-x)); }
+IADMM_DEV float tanh_cell(float x) {
+  const float ax = fabsf(x);
+  const float s = x * x;
+  float p = fmaf(s, -0.0057040372917676625f, 0.020637863933015994f);
+  p = fmaf(s, p, -0.05373916009365762f);
+  p = fmaf(s, p, 0.13331431844163766f);
+  p = fmaf(s, p, -0.3333328129024227f);
+  const float small = fmaf(x * s, p, x);
+  const float e = __expf(2.0f * ax);
+  const float big = 1.0f - 2.0f * __builtin_amdgcn_rcpf(e + 1.0f);
+  return ax < 0.625f ? small : copysignf(big, x);
+}
+
 IADMM_DEV float get4(const float4& v, int e) {
   return e == 0 ? v.x : (e == 1 ? v.y : (e == 2 ? v.z : v.w));
 }

@@ -12,9 +12,11 @@
 // gates at the same register index: the whole cell update runs in registers in the epilogue.
 //
 // Tile: workgroup = 4 waves = 32 hidden units x 256 rows; wave = 32 hidden x 64 rows x 4 gates
-// (8 accumulators of 32x32 = 128 acc registers).  K is staged in chunks of 32 through padded LDS
-// (row stride 36 floats: conflict-free ds_read_b128 for 16 distinct rows), with the next chunk
-// prefetched into registers while the MFMAs run.  Workgroups are remapped XCD-aware so the njt
+// (8 accumulators of 32x32 = 128 acc registers).  K is staged in 16-deep chunks through a 3-stage
+// LDS ring filled by LDS-DMA (buffer_load_dwordx4 ... lds; cell_tile.h cell_mainloop_dma), one
+// barrier per chunk, fragments double-buffered in registers; the epilogue's C / xv / g operands are
+// loaded behind the last chunk's MFMAs.  (h % 4 != 0 or unaligned rows: the register-staged
+// 32-deep loop, cell_mainloop, same products in the same order.)  Workgroups are remapped XCD-aware so the njt
 // hidden tiles of one 256-row H panel run back to back on the same XCD (panel read from HBM once,
 // then served by that XCD's L2).
 #include "cell_tile.h"
@@ -102,9 +104,11 @@ extern "C" int iadmm_lstm_cell_fwd(int64_t M, int64_t h, const float* H, const f
   CellArgsT a{M, (int)h, (int)njt, (int)cdiv(h, kBK), H, C, xv, g, Upk, Wx, Hn, Cn, part};
   const bool vec = (h % 4 == 0) && aligned16(H) && aligned16(C) && aligned16(Hn) && aligned16(Cn);
   const dim3 grid((unsigned)(nrt * njt));
-  if (vec)
-    hipLaunchKernelGGL((cell_fwd_kernel<true, 4, 0>), grid, dim3(256), 0, (hipStream_t)stream, a);
-  else
+  if (vec) {
+    // LDS-DMA main loop (cell_tile.h cell_mainloop_dma): 74 KiB of dynamic LDS per workgroup
+    IADMM_ALLOW_LDS(cell_fwd_dma_kernel<0>, kDmaLdsBytes);
+    hipLaunchKernelGGL((cell_fwd_dma_kernel<0>), grid, dim3(256), kDmaLdsBytes, (hipStream_t)stream, a);
+  } else
     hipLaunchKernelGGL((cell_fwd_kernel<false, 4, 0>), grid, dim3(256), 0, (hipStream_t)stream, a);
   IADMM_CHECK_LAUNCH();
   return 0;

@@ -216,10 +216,10 @@ __global__ __launch_bounds__(256, 2) void cell_f16x3_kernel(CellF16x3Args a) {
           const float xw = in0 * get4(wv[3 * g], e) + in1 * get4(wv[3 * g + 1], e);
           pre[g] = (xw + acc[g][r][q] * inv) + get4(wv[3 * g + 2], e);
         }
-        const float ig = sigmoidf_(pre[0]), fg = sigmoidf_(pre[1]), og = sigmoidf_(pre[2]);
-        const float ug = tanhf(pre[3]);
+        const float ig = sigmoid_cell(pre[0]), fg = sigmoid_cell(pre[1]), og = sigmoid_cell(pre[2]);
+        const float ug = tanh_cell(pre[3]);
         const float c2 = ig * ug + fg * get4(cold, e);
-        const float h2 = og * tanhf(c2);
+        const float h2 = og * tanh_cell(c2);
         set4(cnew, e, c2);
         set4(hnew, e, h2);
         const _Float16 hi = (_Float16)h2;

@@ -183,11 +183,11 @@ __global__ __launch_bounds__(256, 2) void lstm_cell_bwd_kernel(CellBwdArgs a) {
           const float xw = in0 * get4(wv[3 * g], e) + in1 * get4(wv[3 * g + 1], e);
           pre[g] = (xw + acc[g][r][q]) + get4(wv[3 * g + 2], e);
         }
-        const float ig = sigmoidf_(pre[0]), fg = sigmoidf_(pre[1]), og = sigmoidf_(pre[2]);
-        const float ug = tanhf(pre[3]);
+        const float ig = sigmoid_cell(pre[0]), fg = sigmoid_cell(pre[1]), og = sigmoid_cell(pre[2]);
+        const float ug = tanh_cell(pre[3]);
         const float cin = get4(cin4, e);
         const float c2 = ig * ug + fg * cin;
-        const float tc = tanhf(c2);
+        const float tc = tanh_cell(c2);
         const float h2 = og * tc;
         const float wh = get4(wv[12], e);
         const float dHt = get4(dh4, e) + dq * wh;

@@ -82,11 +82,22 @@ struct Variant {
   void (*launch)(CellArgsT, int64_t, hipStream_t);
 };
 
-template <int NW, int PRIO>
+template <int NW, int PRIO, bool BUF = false>
 void launch_v(CellArgsT a, int64_t M, hipStream_t s) {
   const int64_t rows = 64 * NW;
   const int64_t nrt = (M + rows - 1) / rows;
-  hipLaunchKernelGGL((cell_fwd_kernel<true, NW, PRIO>), dim3((unsigned)(nrt * a.njt)), dim3(64 * NW), 0, s, a);
+  hipLaunchKernelGGL((cell_fwd_kernel<true, NW, PRIO, BUF>), dim3((unsigned)(nrt * a.njt)), dim3(64 * NW), 0, s, a);
+}
+
+template <int DIAG>
+void launch_dma(CellArgsT a, int64_t M, hipStream_t s) {
+  static bool once = [] {
+    CK(hipFuncSetAttribute((const void*)cell_fwd_dma_kernel<DIAG>, hipFuncAttributeMaxDynamicSharedMemorySize, kDmaLdsBytes));
+    return true;
+  }();
+  (void)once;
+  const int64_t nrt = (M + 255) / 256;
+  hipLaunchKernelGGL(cell_fwd_dma_kernel<DIAG>, dim3((unsigned)(nrt * a.njt)), dim3(256), kDmaLdsBytes, s, a);
 }
 
 int main(int argc, char** argv) {
@@ -110,10 +121,9 @@ int main(int argc, char** argv) {
   CellArgsT a{M, (int)h, njt, nkc32, H, C, xv, g, Upk, Wx, Hn, Cn, part};
   std::vector<Variant> vs = {
       {"NW4 (production)        ", launch_v<4, 0>},
-      {"NW4 setprio per cluster ", launch_v<4, 1>},
-      {"NW8                     ", launch_v<8, 0>},
-      {"NW8 setprio per cluster ", launch_v<8, 1>},
-      {"NW8 static prio waves4-7", launch_v<8, 2>},
+      {"NW4 buffer-load H       ", launch_v<4, 0, true>},
+      {"LDS-DMA ring BK16 x3    ", launch_dma<0>},
+      {"DIAG: DMA, no epilogue  ", launch_dma<1>},
   };
   const double flop = (8.0 * h * h + 18.0 * h) * M;
   hipStream_t s;
@@ -142,6 +152,7 @@ int main(int argc, char** argv) {
     CK(hipMemcpyAsync(p1.data(), part, p1.size() * 4, hipMemcpyDeviceToHost, s));
     CK(hipStreamSynchronize(s));
     for (size_t i = 1; i < vs.size(); ++i) {
+      if (vs[i].name.rfind("DIAG", 0) == 0) continue;
       vs[i].launch(a, M, s);
       CK(hipMemcpyAsync(h2.data(), Hn, h2.size() * 4, hipMemcpyDeviceToHost, s));
       CK(hipMemcpyAsync(p2.data(), part, p2.size() * 4, hipMemcpyDeviceToHost, s));
