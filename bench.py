@@ -216,7 +216,7 @@ def main():
             "final_residual": {"primal_mean": primal, "dual_mean": dual, "sum": primal + dual},
             "roofline": {"kernel": "iadmm_lstm_cell_fwd", "bound": "mfma", "achieved": cell_tf,
                          "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": cell_tf / FP32_MFMA_PEAK_TFLOPS,
-                         "traffic": pmc_traffic(("cell_fwd_kernel<", "lstm_cell_kernel"), n, mi + me, h, B),
+                         "traffic": pmc_traffic(("cell_fwd_dma_kernel",), n, mi + me, h, B),
                          "traffic_source": "profiles/r*_pmc_{FETCH,WRITE}_SIZE_*.csv (separate --pmc passes)",
                          "avg_launch_ms": ms_cell, "launches": n_cell,
                          "algorithmic_per_launch": cell_flop},

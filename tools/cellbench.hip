@@ -97,7 +97,7 @@ void launch_dma(CellArgsT a, int64_t M, hipStream_t s) {
   }();
   (void)once;
   const int64_t nrt = (M + 255) / 256;
-  hipLaunchKernelGGL(cell_fwd_dma_kernel<DIAG>, dim3((unsigned)(nrt * a.njt)), dim3(256), kDmaLdsBytes, s, a);
+  hipLaunchKernelGGL((cell_fwd_dma_kernel<DIAG>), dim3((unsigned)(nrt * a.njt)), dim3(256), kDmaLdsBytes, s, a);
 }
 
 int main(int argc, char** argv) {
