@@ -280,7 +280,7 @@ IADMM_DEV void cell_mainloop_dma(const float* __restrict__ H, int64_t M, int h, 
 }
 
 // The fused cell epilogue: gates, C' = I U + F C, H' = O tanh(C'), projection partial, from the
-// accumulators of a 32-unit x (wave's 64 rows) tile.  sW = the tile's Wx rows ([32 units][16 fields]).
+// accumulators of a 32-unit x (wave's 64 rows) tile.
 // Split in two so a kernel can issue the global loads (cell_epi_load) early, e.g. before its last
 // K chunk, and keep them in registers until cell_epi_compute.
 // accumulator element q of lane (jl,hf): hidden jj = (q&3) + 8*(q>>2) + 4*hf, data row jl.
@@ -312,8 +312,19 @@ IADMM_DEV void cell_epi_load(const CellArgsT& a, int jt, int64_t rbase, int wave
   }
 }
 
-template <bool VEC>
-IADMM_DEV void cell_epi_compute(const CellArgsT& a, floatx16 (&acc)[4][2], const float* sW, int jt,
+// Packed epilogue: unit pairs (jj, jj+1) go through v_pk_*_f32 together (common.h *_cell2).
+// sWp = the tile's Wx fields as [16 unit pairs][16 fields][2 units] (cell_fill_wpairs), so one
+// float4 holds two fields of both units of a pair.  The projection partial runs as two interleaved
+// sums (even / odd unit of each pair) added at the end.
+IADMM_DEV void cell_fill_wpairs(const float* __restrict__ Wx, int jt, float* sWp, int tid, int nthreads) {
+  for (int i = tid; i < kWxF * kJT; i += nthreads) {
+    const int pr = i >> 5, f = (i >> 1) & 15, u = i & 1;
+    sWp[i] = Wx[(int64_t)(jt * kJT + 2 * pr + u) * kWxF + f];
+  }
+}
+
+template <bool VEC, int DIAG = 0>
+IADMM_DEV void cell_epi_compute(const CellArgsT& a, floatx16 (&acc)[4][2], const float* sWp, int jt,
                                 int64_t rbase, int wave, int jl, int hf, const CellEpiIn& ei) {
   const int h = a.h;
   const int64_t M = a.M;
@@ -321,8 +332,8 @@ IADMM_DEV void cell_epi_compute(const CellArgsT& a, floatx16 (&acc)[4][2], const
   for (int r = 0; r < 2; ++r) {
     const int64_t R = rbase + wave * 64 + r * 32 + jl;
     const bool rok = R < M;
-    const float in0 = ei.in0[r], in1 = ei.in1[r];
-    float gsum = 0.f;
+    const float2v in0 = splat2(ei.in0[r]), in1 = splat2(ei.in1[r]);
+    float2v gs = splat2(0.f);
 #pragma unroll
     for (int qq = 0; qq < 4; ++qq) {
       __builtin_amdgcn_sched_barrier(0);  // one (rows, 4 units) group at a time: bounded live range
@@ -331,31 +342,36 @@ IADMM_DEV void cell_epi_compute(const CellArgsT& a, floatx16 (&acc)[4][2], const
       const float4 cold = ei.cold[r][qq];
       float4 cnew, hnew;
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int q = qq * 4 + e;
-        // unit jj0+e: its 16 packed fields (Wx layout), one 64-B row of sW (same address across
-        // the 32 lanes of a half-wave: broadcast)
-        float wf[16];
+      for (int pp = 0; pp < 2; ++pp) {
+        // fields 0..13 of units (jj0 + 2pp, +1): 7 float4 of one 128-B sWp row (broadcast across
+        // the 32 lanes of a half-wave)
+        const float4* wp = reinterpret_cast<const float4*>(sWp + ((jj0 >> 1) + pp) * 32);
+        float4 w4[7];
 #pragma unroll
-        for (int f4 = 0; f4 < 4; ++f4) {
-          const float4 t = *reinterpret_cast<const float4*>(&sW[(jj0 + e) * kWxF + 4 * f4]);
-          wf[4 * f4] = t.x; wf[4 * f4 + 1] = t.y; wf[4 * f4 + 2] = t.z; wf[4 * f4 + 3] = t.w;
-        }
-        float pre[4];
+        for (int i = 0; i < 7; ++i) w4[i] = wp[i];
+        auto fld = [&](int f) -> float2v {
+          const float4& t = w4[f >> 1];
+          return (f & 1) ? float2v{t.z, t.w} : float2v{t.x, t.y};
+        };
+        const int q = qq * 4 + 2 * pp;
+        float2v pre[4];
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
-          const float xw = in0 * wf[3 * g] + in1 * wf[3 * g + 1];
-          pre[g] = (xw + acc[g][r][q]) + wf[3 * g + 2];
+          const float2v xw = in0 * fld(3 * g) + in1 * fld(3 * g + 1);
+          pre[g] = (xw + float2v{acc[g][r][q], acc[g][r][q + 1]}) + fld(3 * g + 2);
         }
-        const float ig = sigmoid_cell(pre[0]), fg = sigmoid_cell(pre[1]), og = sigmoid_cell(pre[2]);
-        const float ug = tanh_cell(pre[3]);
-        const float c2 = ig * ug + fg * get4(cold, e);
-        const float h2 = og * tanh_cell(c2);
-        set4(cnew, e, c2);
-        set4(hnew, e, h2);
-        gsum = fmaf(h2, wf[12], gsum);
+        const float2v ig = sigmoid_cell2(pre[0]), fg = sigmoid_cell2(pre[1]), og = sigmoid_cell2(pre[2]);
+        const float2v ug = tanh_cell2(pre[3]);
+        const float2v cv = pp ? float2v{cold.z, cold.w} : float2v{cold.x, cold.y};
+        const float2v c2 = ig * ug + fg * cv;
+        const float2v h2 = og * tanh_cell2(c2);
+        gs = fma2(h2, fld(12), gs);
+        if (pp == 0) { cnew.x = c2.x; cnew.y = c2.y; hnew.x = h2.x; hnew.y = h2.y; }
+        else         { cnew.z = c2.x; cnew.w = c2.y; hnew.z = h2.x; hnew.w = h2.y; }
       }
-      if (rok) {
+      if (DIAG == 2) {  // timing diagnostic: no H'/C' stores (keep the values alive)
+        gs.x += cnew.x + cnew.y + cnew.z + cnew.w;
+      } else if (rok) {
         if constexpr (VEC) {
           if (j0 < h) {
             *reinterpret_cast<float4*>(a.Cn + R * h + j0) = cnew;
@@ -372,6 +388,7 @@ IADMM_DEV void cell_epi_compute(const CellArgsT& a, floatx16 (&acc)[4][2], const
         }
       }
     }
+    float gsum = gs.x + gs.y;
     gsum += __shfl_xor(gsum, 32, 64);
     if (hf == 0 && rok) a.part[(int64_t)jt * M + R] = gsum;
   }
@@ -402,7 +419,7 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void cell_fwd_kernel(Cell
   const int64_t M = a.M;
   const int64_t rbase = (int64_t)rt * ROWS;
 
-  for (int i = tid; i < kWxF * kJT; i += 64 * NW) sW[i] = a.Wx[(int64_t)jt * kJT * kWxF + i];
+  cell_fill_wpairs(a.Wx, jt, sW, tid, 64 * NW);
 
   floatx16 acc[4][2];
   cell_mainloop<VEC, NW, PRIO, BUF>(a.H, M, h, a.nkc32, a.Upk + (int64_t)jt * a.nkc32 * 128 * kBK, rbase, sA, sB,
@@ -414,10 +431,16 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void cell_fwd_kernel(Cell
 
 // Forward cell kernel on the LDS-DMA main loop (VEC only: h % 4 == 0, 16-B aligned rows).
 // Dynamic LDS: kRingFloats + kWxF*kJT floats (74 KiB) -> 2 workgroups per CU.
-// DIAG (timing tools only): 1 = skip the epilogue (main-loop cost).
+// DIAG (timing tools only): 1 = skip the epilogue (main-loop cost); 2 = epilogue without the
+// H'/C' stores; 3 = epilogue without the C / xv / g loads.
+// DIAG 4: as 0, plus s_memtime stamps (kernel start, main loop end, epilogue operands landed,
+// epilogue end) of wave 0 of every workgroup into a.part[njt * M ...]; 5: same without the H'/C'
+// stores -- diagnostic builds only (tools/cellbench).
 template <int DIAG = 0>
 __global__ __launch_bounds__(256, 2) void cell_fwd_dma_kernel(CellArgsT a) {
   extern __shared__ __attribute__((aligned(16))) float dsm[];
+  uint64_t t_start = 0, t_ml = 0;
+  if constexpr (DIAG == 4) t_start = __builtin_amdgcn_s_memtime();
   float* ring = dsm;
   float* sW = dsm + kRingFloats;
   int jt, rt;
@@ -426,11 +449,22 @@ __global__ __launch_bounds__(256, 2) void cell_fwd_dma_kernel(CellArgsT a) {
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int jl = lane & 31, hf = lane >> 5;
   const int64_t rbase = (int64_t)rt * kRows;
-  for (int i = tid; i < kWxF * kJT; i += 256) sW[i] = a.Wx[(int64_t)jt * kJT * kWxF + i];
+  cell_fill_wpairs(a.Wx, jt, sW, tid, 256);
   floatx16 acc[4][2];
   CellEpiIn ei;
   cell_mainloop_dma(a.H, a.M, a.h, a.nkc32, a.Upk + (int64_t)jt * a.nkc32 * 128 * kBK, rbase, ring, acc,
-                    tid, wave, jl, hf, [&] { cell_epi_load<true>(a, jt, rbase, wave, jl, hf, ei); });
+                    tid, wave, jl, hf, [&] {
+                      if constexpr (DIAG == 3) {
+#pragma unroll
+                        for (int r = 0; r < 2; ++r) {
+                          ei.in0[r] = ei.in1[r] = 0.5f;
+#pragma unroll
+                          for (int qq = 0; qq < 4; ++qq) ei.cold[r][qq] = make_float4(0.1f, 0.2f, 0.3f, 0.4f);
+                        }
+                      } else {
+                        cell_epi_load<true>(a, jt, rbase, wave, jl, hf, ei);
+                      }
+                    });
   if constexpr (DIAG == 1) {
     float t = 0.f;
 #pragma unroll
@@ -443,7 +477,20 @@ __global__ __launch_bounds__(256, 2) void cell_fwd_dma_kernel(CellArgsT a) {
     return;
   }
   __syncthreads();  // sW visible (written before the main loop)
-  cell_epi_compute<true>(a, acc, sW, jt, rbase, wave, jl, hf, ei);
+  uint64_t t_c = 0;
+  if constexpr (DIAG >= 4) {
+    t_ml = __builtin_amdgcn_s_memtime();
+    vm_wait<0>();  // the prefetched epilogue operands
+    t_c = __builtin_amdgcn_s_memtime();
+  }
+  cell_epi_compute<true, DIAG == 4 ? 0 : (DIAG == 5 ? 2 : DIAG)>(a, acc, sW, jt, rbase, wave, jl, hf, ei);
+  if constexpr (DIAG >= 4) {
+    const uint64_t t_end = __builtin_amdgcn_s_memtime();
+    if (tid == 0) {
+      uint64_t* st = reinterpret_cast<uint64_t*>(a.part + (int64_t)a.njt * a.M) + (int64_t)blockIdx.x * 4;
+      st[0] = t_start; st[1] = t_ml; st[2] = t_c; st[3] = t_end;
+    }
+  }
 }
 constexpr int kDmaLdsBytes = (kRingFloats + kWxF * kJT) * 4;
 

@@ -108,7 +108,7 @@ int main(int argc, char** argv) {
   const int njt = (h + 31) / 32, nkc32 = (h + 31) / 32;
   float *H, *C, *xv, *g, *Upk, *Wx, *Hn, *Cn, *part;
   CK(hipMalloc(&H, M * h * 4)); CK(hipMalloc(&C, M * h * 4)); CK(hipMalloc(&Hn, M * h * 4)); CK(hipMalloc(&Cn, M * h * 4));
-  CK(hipMalloc(&xv, M * 4)); CK(hipMalloc(&g, M * 4)); CK(hipMalloc(&part, (int64_t)njt * M * 4));
+  CK(hipMalloc(&xv, M * 4)); CK(hipMalloc(&g, M * 4)); CK(hipMalloc(&part, (int64_t)njt * M * 4 + (int64_t)njt * ((M + 255) / 256) * 32));
   const int64_t nup = (int64_t)njt * nkc32 * 128 * 32, nwx = (int64_t)njt * 32 * 16;
   CK(hipMalloc(&Upk, nup * 4)); CK(hipMalloc(&Wx, nwx * 4));
   hipLaunchKernelGGL(fill, dim3(4096), dim3(256), 0, 0, H, M * h, 1u, 0.9f);
@@ -123,7 +123,11 @@ int main(int argc, char** argv) {
       {"NW4 (production)        ", launch_v<4, 0>},
       {"NW4 buffer-load H       ", launch_v<4, 0, true>},
       {"LDS-DMA ring BK16 x3    ", launch_dma<0>},
+      {"DIAG: DMA + stamps      ", launch_dma<4>},
+      {"DIAG: stamps, no stores ", launch_dma<5>},
       {"DIAG: DMA, no epilogue  ", launch_dma<1>},
+      {"DIAG: DMA, no H/C stores", launch_dma<2>},
+      {"DIAG: DMA, no C loads   ", launch_dma<3>},
   };
   const double flop = (8.0 * h * h + 18.0 * h) * M;
   hipStream_t s;
@@ -164,6 +168,23 @@ int main(int argc, char** argv) {
     }
   }
   printf("M=%lld h=%lld rounds=%d\n", (long long)M, (long long)h, rounds);
+  for (int dv : {4, 5}) {  // per-workgroup phase lengths (s_memtime cycles) from the stamped variants
+    const int64_t nwg = njt * ((M + 255) / 256);
+    if (dv == 4) launch_dma<4>(a, M, s); else launch_dma<5>(a, M, s);
+    CK(hipStreamSynchronize(s));
+    std::vector<uint64_t> st(nwg * 4);
+    CK(hipMemcpy(st.data(), reinterpret_cast<char*>(part) + (int64_t)njt * M * 4, nwg * 32, hipMemcpyDeviceToHost));
+    std::vector<double> ml, cw, ep;
+    for (int64_t w = 0; w < nwg; ++w) {
+      ml.push_back((double)(st[4 * w + 1] - st[4 * w]));
+      cw.push_back((double)(st[4 * w + 2] - st[4 * w + 1]));
+      ep.push_back((double)(st[4 * w + 3] - st[4 * w + 2]));
+    }
+    std::sort(ml.begin(), ml.end()); std::sort(cw.begin(), cw.end()); std::sort(ep.begin(), ep.end());
+    printf("stamps DIAG %d: main loop median %.0f cyc (p10 %.0f p90 %.0f) | operand wait median %.0f (p90 %.0f) | "
+           "epilogue compute+store median %.0f (p10 %.0f p90 %.0f)\n", dv,
+           ml[nwg / 2], ml[nwg / 10], ml[9 * nwg / 10], cw[nwg / 2], cw[9 * nwg / 10], ep[nwg / 2], ep[nwg / 10], ep[9 * nwg / 10]);
+  }
   {  // MFMA ceiling: 512 blocks x 4 waves, each wave 8 x 32x32x2 (or 32 x 16x16x4) per iteration
     const int iters = 20000, blocks = 512;
     for (int shape : {32, 33, 32, 33}) {

@@ -10,13 +10,21 @@
 
 using namespace iadmm;
 
-__global__ void eval(int64_t n, const float* x, float* out) {
+__global__ void eval(int64_t n, const float* x, float* out, unsigned* packed_mismatch) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     const float v = x[i];
     out[4 * i + 0] = sigmoid_cell(v);
     out[4 * i + 1] = sigmoidf_(v);
     out[4 * i + 2] = tanh_cell(v);
     out[4 * i + 3] = tanhf(v);
+    // the packed forms must reproduce the scalar ones bit for bit
+    const float w = x[(i + 1) % n];
+    const float2v sp = sigmoid_cell2(float2v{v, w}), tp = tanh_cell2(float2v{v, w});
+    const bool bad = __float_as_uint(sp.x) != __float_as_uint(sigmoid_cell(v)) ||
+                     __float_as_uint(sp.y) != __float_as_uint(sigmoid_cell(w)) ||
+                     __float_as_uint(tp.x) != __float_as_uint(tanh_cell(v)) ||
+                     __float_as_uint(tp.y) != __float_as_uint(tanh_cell(w));
+    if (bad) atomicAdd(packed_mismatch, 1u);
   }
 }
 
@@ -37,9 +45,14 @@ int main() {
   (void)lo; (void)hi;
   const int64_t n = xs.size();
   float *dx, *dout;
-  hipMalloc(&dx, n * 4); hipMalloc(&dout, n * 16);
+  unsigned* dbad;
+  hipMalloc(&dx, n * 4); hipMalloc(&dout, n * 16); hipMalloc(&dbad, 4);
+  hipMemset(dbad, 0, 4);
   hipMemcpy(dx, xs.data(), n * 4, hipMemcpyHostToDevice);
-  hipLaunchKernelGGL(eval, dim3(4096), dim3(256), 0, 0, n, dx, dout);
+  hipLaunchKernelGGL(eval, dim3(4096), dim3(256), 0, 0, n, dx, dout, dbad);
+  unsigned bad = 0;
+  hipMemcpy(&bad, dbad, 4, hipMemcpyDeviceToHost);
+  printf("packed vs scalar forms: %u mismatching points\n", bad);
   std::vector<float> out(4 * n);
   hipMemcpy(out.data(), dout, n * 16, hipMemcpyDeviceToHost);
   const char* names[4] = {"sigmoid_cell", "sigmoidf_ (1/(1+expf))", "tanh_cell", "tanhf (ocml)"};
