@@ -153,14 +153,19 @@ IADMM_DEV void vm_wait() {  // s_waitcnt vmcnt(N), other counters untouched (gfx
   __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
 }
 
-// acc[g][r] as cell_mainloop; Ubase = Upk + jt*nkc32*128*32 (fp32 32-deep packing), ring = LDS.
+// acc[g][r] += A[g*32 + .., k] . B[wave*64 + r*32 + .., k] over k < K, through the LDS ring.
+//   B: row-major panel (row stride ldb floats) starting at the workgroup's first row; rows past
+//      nb_valid and k past K read as zero (buffer range check / out-of-range offset).
+//   A: 128 rows.  A_PACKED: the fp32 32-deep packing of lstm_pack_kernel (Ubase = Upk +
+//      jt*nkc32*128*32, zero-padded, nkc32 = ceil(K/32)); otherwise row-major, row stride lda, rows
+//      past na_valid and k past K zero.
 // before_last() runs once, just before the last chunk's MFMAs (e.g. to prefetch epilogue operands
 // behind them).
-template <class BeforeLast>
-IADMM_DEV void cell_mainloop_dma(const float* __restrict__ H, int64_t M, int h, int nkc32,
-                                 const float* __restrict__ Ubase, int64_t rbase, float* ring,
-                                 floatx16 (&acc)[4][2], int tid, int wave, int jl, int hf,
-                                 BeforeLast&& before_last) {
+template <bool A_PACKED, class BeforeLast>
+IADMM_DEV void mainloop_dma(const float* __restrict__ Abase, int na_valid, int lda,
+                            const float* __restrict__ Bbase, int64_t nb_valid, int ldb, int K,
+                            float* ring, floatx16 (&acc)[4][2], int tid, int wave, int jl, int hf,
+                            BeforeLast&& before_last) {
 #pragma unroll
   for (int g = 0; g < 4; ++g)
 #pragma unroll
@@ -169,43 +174,53 @@ IADMM_DEV void cell_mainloop_dma(const float* __restrict__ H, int64_t M, int h, 
       for (int q = 0; q < 16; ++q) acc[g][r][q] = 0.f;
 
   const int lane = tid & 63;
-  const int nk = (h + kBKd - 1) / kBKd;
-  const int64_t nvalid = (M - rbase) < 256 ? (M - rbase) : 256;
+  const int nk = (K + kBKd - 1) / kBKd;
+  const int nkc32 = (K + kBK - 1) / kBK;
+  const int64_t nbv = nb_valid < 256 ? nb_valid : 256;
   const __amdgpu_buffer_rsrc_t hrs = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<float*>(H + rbase * h), 0, (int)(nvalid * h * 4), 0x00020000);
+      const_cast<float*>(Bbase), 0, (int)(nbv * ldb * 4), 0x00020000);
   const __amdgpu_buffer_rsrc_t urs = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<float*>(Ubase), 0, nkc32 * 128 * kBK * 4, 0x00020000);
+      const_cast<float*>(Abase), 0,
+      A_PACKED ? nkc32 * 128 * kBK * 4 : (na_valid < 128 ? na_valid : 128) * lda * 4, 0x00020000);
 
   // Per-lane source offsets of this wave's pieces (piece = 16 LDS rows x 4 slots).
   const int prow = lane >> 2, pslot = lane & 3;
   unsigned aoff[2];
+  int ak4[2];
   int bk4[4];
   unsigned boff[4];
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
     const int row = (wave * 2 + i) * 16 + prow;             // g*32 + jj
     const int c = pslot ^ ((row >> 2) & 3);
-    aoff[i] = (unsigned)(row * kBK + c * 4) * 4u;            // + kc32*16 KiB + half*64 B
+    ak4[i] = c * 4;
+    aoff[i] = A_PACKED ? (unsigned)(row * kBK + c * 4) * 4u    // + kc32*16 KiB + half*64 B
+                       : (unsigned)(row * lda + c * 4) * 4u;   // + kc*64 B
   }
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int row = (wave * 4 + i) * 16 + prow;
     const int c = pslot ^ ((row >> 2) & 3);
     bk4[i] = c * 4;
-    boff[i] = (unsigned)(row * h + c * 4) * 4u;              // + kc*64 B
+    boff[i] = (unsigned)(row * ldb + c * 4) * 4u;            // + kc*64 B
   }
   auto issue = [&](int kc) {
     const int st = kc % kStages;
     float* sa = ring + st * (kStageA + kStageB);
     float* sb = sa + kStageA;
-    const unsigned ua = (unsigned)((kc >> 1) * 128 * kBK + (kc & 1) * kBKd) * 4u;
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(urs, (lds_void*)(sa + (wave * 2 + i) * 256), 16,
-                                               aoff[i] + ua, 0, 0, 0);
+    for (int i = 0; i < 2; ++i) {
+      unsigned o;
+      if constexpr (A_PACKED) {
+        o = aoff[i] + (unsigned)((kc >> 1) * 128 * kBK + (kc & 1) * kBKd) * 4u;
+      } else {
+        o = (kc * kBKd + ak4[i] < K) ? aoff[i] + (unsigned)(kc * kBKd * 4) : 0x80000000u;
+      }
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(urs, (lds_void*)(sa + (wave * 2 + i) * 256), 16, o, 0, 0, 0);
+    }
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      const unsigned o = (kc * kBKd + bk4[i] < h) ? boff[i] + (unsigned)(kc * kBKd * 4) : 0x80000000u;
+      const unsigned o = (kc * kBKd + bk4[i] < K) ? boff[i] + (unsigned)(kc * kBKd * 4) : 0x80000000u;
       __builtin_amdgcn_raw_ptr_buffer_load_lds(hrs, (lds_void*)(sb + (wave * 4 + i) * 256), 16, o, 0, 0, 0);
     }
   };
@@ -277,6 +292,18 @@ IADMM_DEV void cell_mainloop_dma(const float* __restrict__ H, int64_t M, int h, 
   __builtin_amdgcn_sched_barrier(0);
   mma(fa0, fb0);
   mma(fa1, fb1);
+}
+
+// The cell's instance: A = the packed gate weights of hidden tile jt, B = the H panel of rows
+// [rbase, rbase + 256).
+template <class BeforeLast>
+IADMM_DEV void cell_mainloop_dma(const float* __restrict__ H, int64_t M, int h, int nkc32,
+                                 const float* __restrict__ Ubase, int64_t rbase, float* ring,
+                                 floatx16 (&acc)[4][2], int tid, int wave, int jl, int hf,
+                                 BeforeLast&& before_last) {
+  (void)nkc32;
+  mainloop_dma<true>(Ubase, 128, kBK, H + rbase * h, M - rbase, h, h, ring, acc, tid, wave, jl, hf,
+                     before_last);
 }
 
 // The fused cell epilogue: gates, C' = I U + F C, H' = O tanh(C'), projection partial, from the

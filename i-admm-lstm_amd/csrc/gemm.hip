@@ -4,17 +4,16 @@
 //   gemm_tn : out[Ni, No]  = X[M, Ni]^T . Y[M, No]      (dU_cat = H^T . dP, split over M)
 //
 // gemm_nt uses the forward cell kernel's tiling (workgroup = 128 outputs x 256 rows, wave = 128
-// outputs x 64 rows = 8 accumulators of v_mfma_f32_32x32x2_f32, K staged 32-deep through padded
-// LDS, one 16-B LDS read per operand fragment).  gemm_tn contracts over the long row dimension:
+// outputs x 64 rows = 8 accumulators of v_mfma_f32_32x32x2_f32) and, for K % 4 == 0 with aligned
+// operands, its LDS-DMA main loop (cell_tile.h mainloop_dma); otherwise K is staged 32-deep
+// through padded LDS by registers.  gemm_tn contracts over the long row dimension:
 // a workgroup owns a 128 x 128 output tile and a contiguous slice of rows, stages [32 rows x 128]
 // of both operands in LDS (both are row-major along the output dims, so one fragment element per
 // lane is a conflict-free ds_read_b32) and writes an fp32 partial slab; iadmm_slab_reduce sums the
 // slabs in a fixed order (deterministic, no atomics).
-#include "common.h"
+#include "cell_tile.h"
 
 namespace iadmm {
-
-typedef float floatx16 __attribute__((ext_vector_type(16)));
 
 constexpr int kGBK = 32;
 constexpr int kGLD = kGBK + 4;
@@ -122,6 +121,50 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(int64_t M, int Ni, int 
   }
 }
 
+// gemm_nt on the LDS-DMA main loop of the cell kernel (cell_tile.h mainloop_dma, A row-major):
+// K % 4 == 0 and 16-B aligned operands.  Workgroups remapped XCD-aware like the cell kernel so the
+// output tiles of one 256-row X panel run back to back on one XCD (panel reused from its L2).
+template <bool ACC>
+__global__ __launch_bounds__(256, 2) void gemm_nt_dma_kernel(int64_t M, int Ni, int K, const float* X,
+                                                             const float* W, float* out) {
+  extern __shared__ __attribute__((aligned(16))) float ring[];
+  const int nit = (Ni + 127) / 128;
+  int it, rti;
+  cell_tile_of_block(nit, it, rti);
+  const int64_t rt = rti;
+  const int tid = threadIdx.x, lane = tid & 63, jl = lane & 31, hf = lane >> 5;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int i0 = it * 128;
+  const int64_t r0 = rt * 256;
+  floatx16 acc[4][2];
+  mainloop_dma<false>(W + (int64_t)i0 * K, Ni - i0, K, X + r0 * K, M - r0, K, K, ring, acc, tid, wave, jl, hf,
+                      [] {});
+#pragma unroll
+  for (int r = 0; r < 2; ++r) {
+    const int64_t R = r0 + wave * 64 + r * 32 + jl;
+    if (R >= M) continue;
+#pragma unroll
+    for (int g = 0; g < 4; ++g)
+#pragma unroll
+      for (int qq = 0; qq < 4; ++qq) {
+        const int ib = i0 + g * 32 + 8 * qq + 4 * hf;
+        float* o = out + R * Ni + ib;
+        if (ib + 3 < Ni) {
+          float4 v = make_float4(acc[g][r][4 * qq], acc[g][r][4 * qq + 1], acc[g][r][4 * qq + 2], acc[g][r][4 * qq + 3]);
+          if (ACC) {
+            const float4 p = *reinterpret_cast<const float4*>(o);
+            v.x += p.x; v.y += p.y; v.z += p.z; v.w += p.w;
+          }
+          *reinterpret_cast<float4*>(o) = v;
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            if (ib + e < Ni) o[e] = ACC ? o[e] + acc[g][r][4 * qq + e] : acc[g][r][4 * qq + e];
+        }
+      }
+  }
+}
+
 // Partial slab of X[rows, Ni]^T . Y[rows, No] for the row slice of blockIdx.z.
 __global__ __launch_bounds__(256, 2) void gemm_tn_kernel(int64_t M, int Ni, int No, int64_t rows_per_split,
                                                          const float* X, const float* Y, float* slab) {
@@ -183,6 +226,107 @@ __global__ __launch_bounds__(256, 2) void gemm_tn_kernel(int64_t M, int Ni, int 
       for (int q = 0; q < 16; ++q) {
         const int i = i0 + wi + a * 32 + (q & 3) + 8 * (q >> 2) + 4 * hf;
         const int o = o0 + wo + c * 32 + jl;
+        if (i < Ni && o < No) S[(int64_t)i * No + o] = acc[a][c][q];
+      }
+}
+
+// gemm_tn on an LDS-DMA ring (the cell kernel's pipeline with the contraction over rows):
+// workgroup = 128 (i) x 256 (o) outputs of one row split, wave = 128 (i) x 64 (o) = 4 x 2
+// accumulators of v_mfma_f32_32x32x2_f32.  Per 16-row chunk each wave DMAs 2 pieces of the X
+// panel (2 rows x 128 columns each) and 4 of the Y panel (1 row x 256 columns each) into a 3-stage
+// ring, row-major as in HBM (lane-linear DMA image); fragments are ds_read_b32 of 32 consecutive
+// columns of one row per half-wave (conflict-free without a swizzle).  Rows past the split and
+// columns past Ni / No read as zero (buffer range / out-of-range offsets).  One barrier per chunk;
+// the chunk kc+2 DMA is issued after it, into the stage chunk kc-1 used.  Requires
+// Ni % 4 == No % 4 == 0 and 16-B aligned X, Y.
+constexpr int kTnStageX = 16 * 128, kTnStageY = 16 * 256;
+constexpr int kTnRingFloats = 3 * (kTnStageX + kTnStageY);
+
+__global__ __launch_bounds__(256, 2) void gemm_tn_dma_kernel(int64_t M, int Ni, int No, int64_t rows_per_split,
+                                                             const float* X, const float* Y, float* slab) {
+  extern __shared__ __attribute__((aligned(16))) float ring[];
+  const int tid = threadIdx.x, lane = tid & 63, jl = lane & 31, hf = lane >> 5;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int i0 = blockIdx.x * 128, o0 = blockIdx.y * 256;
+  const int64_t rbeg = (int64_t)blockIdx.z * rows_per_split;
+  const int64_t rend = min(M, rbeg + rows_per_split);
+  const int nrows = (int)(rend - rbeg);
+  const int nk = (nrows + 15) / 16;
+  floatx16 acc[4][2];
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+      for (int q = 0; q < 16; ++q) acc[a][c][q] = 0.f;
+  // panels start at row rbeg; the range ends at the split's last row
+  const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float*>(X + rbeg * Ni), 0, (int)((int64_t)nrows * Ni * 4), 0x00020000);
+  const __amdgpu_buffer_rsrc_t yrs = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float*>(Y + rbeg * No), 0, (int)((int64_t)nrows * No * 4), 0x00020000);
+  // X piece p (1 KiB) = stage rows 2p, 2p+1 (lane >> 5), columns i0 + 4*(lane & 31) .. +4
+  // Y piece q (1 KiB) = stage row q, columns o0 + 4*lane .. +4
+  unsigned xoff[2], yoff[4];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int row = (wave * 2 + i) * 2 + (lane >> 5), col = i0 + (lane & 31) * 4;
+    xoff[i] = (col < Ni) ? (unsigned)(row * Ni + col) * 4u : 0x80000000u;
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int row = wave * 4 + i, col = o0 + lane * 4;
+    yoff[i] = (col < No) ? (unsigned)(row * No + col) * 4u : 0x80000000u;
+  }
+  auto issue = [&](int kc) {
+    float* sx = ring + (kc % 3) * (kTnStageX + kTnStageY);
+    float* sy = sx + kTnStageX;
+    const unsigned ox = (unsigned)(kc * 16 * Ni) * 4u, oy = (unsigned)(kc * 16 * No) * 4u;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(xrs, (lds_void*)(sx + (wave * 2 + i) * 256), 16,
+                                               xoff[i] == 0x80000000u ? xoff[i] : xoff[i] + ox, 0, 0, 0);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(yrs, (lds_void*)(sy + (wave * 4 + i) * 256), 16,
+                                               yoff[i] == 0x80000000u ? yoff[i] : yoff[i] + oy, 0, 0, 0);
+  };
+  auto mma_chunk = [&](int kc) {
+    const float* sx = ring + (kc % 3) * (kTnStageX + kTnStageY);
+    const float* sy = sx + kTnStageX;
+#pragma unroll
+    for (int ks = 0; ks < 8; ++ks) {
+      const int kk = 2 * ks + hf;
+      float av[4], bv[2];
+#pragma unroll
+      for (int a = 0; a < 4; ++a) av[a] = sx[kk * 128 + a * 32 + jl];
+#pragma unroll
+      for (int c = 0; c < 2; ++c) bv[c] = sy[kk * 256 + wave * 64 + c * 32 + jl];
+#pragma unroll
+      for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int c = 0; c < 2; ++c)
+          acc[a][c] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[a], bv[c], acc[a][c], 0, 0, 0);
+    }
+  };
+  issue(0);
+  if (nk > 1) issue(1);
+  for (int kc = 0; kc < nk; ++kc) {
+    if (kc + 1 < nk) vm_wait<6>(); else vm_wait<0>();  // this wave's pieces of chunk kc
+    __builtin_amdgcn_s_barrier();                      // everyone's chunk kc landed; chunk kc-1 read
+    __builtin_amdgcn_sched_barrier(0);
+    if (kc + 2 < nk) issue(kc + 2);
+    mma_chunk(kc);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  float* S = slab + (int64_t)blockIdx.z * Ni * No;
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const int i = i0 + a * 32 + (q & 3) + 8 * (q >> 2) + 4 * hf;
+        const int o = o0 + wave * 64 + c * 32 + jl;
         if (i < Ni && o < No) S[(int64_t)i * No + o] = acc[a][c][q];
       }
 }
@@ -262,7 +406,16 @@ extern "C" int iadmm_gemm_nt(int64_t M, int64_t Ni, int64_t K, const float* X, c
   const dim3 grid((unsigned)(nit * nrt));
   const bool vec = (K % 4 == 0) && (Ni % 4 == 0) && aligned16(X) && aligned16(W) && aligned16(out);
   hipStream_t s = (hipStream_t)stream;
-  if (accumulate) {
+  const bool dma = vec && K * 256 * 4 <= 0x7fffffffLL;  // the DMA kernel's epilogue stores float4 rows
+  if (dma) {
+    if (accumulate) {
+      IADMM_ALLOW_LDS(gemm_nt_dma_kernel<true>, kRingFloats * 4);
+      hipLaunchKernelGGL((gemm_nt_dma_kernel<true>), grid, dim3(256), kRingFloats * 4, s, M, (int)Ni, (int)K, X, W, out);
+    } else {
+      IADMM_ALLOW_LDS(gemm_nt_dma_kernel<false>, kRingFloats * 4);
+      hipLaunchKernelGGL((gemm_nt_dma_kernel<false>), grid, dim3(256), kRingFloats * 4, s, M, (int)Ni, (int)K, X, W, out);
+    }
+  } else if (accumulate) {
     if (vec) hipLaunchKernelGGL((gemm_nt_kernel<true, true>), grid, dim3(256), 0, s, M, (int)Ni, (int)K, X, W, out);
     else hipLaunchKernelGGL((gemm_nt_kernel<true, false>), grid, dim3(256), 0, s, M, (int)Ni, (int)K, X, W, out);
   } else {
@@ -290,8 +443,17 @@ extern "C" int iadmm_gemm_tn(int64_t M, int64_t Ni, int64_t No, int64_t rows_per
     case 3: launch_skinny<3>(M, (int)No, rows_per_split, ns, X, Y, slab, s); break;
     case 4: launch_skinny<4>(M, (int)No, rows_per_split, ns, X, Y, slab, s); break;
     default: {
-      const dim3 grid((unsigned)((Ni + 127) / 128), (unsigned)((No + 127) / 128), (unsigned)ns);
-      hipLaunchKernelGGL(gemm_tn_kernel, grid, dim3(256), 0, s, M, (int)Ni, (int)No, rows_per_split, X, Y, slab);
+      const bool dma = Ni % 4 == 0 && No % 4 == 0 && aligned16(X) && aligned16(Y) && rows_per_split % 16 == 0 &&
+                       rows_per_split * (Ni > No ? Ni : No) * 4 <= 0x7fffffffLL;
+      if (dma) {
+        const dim3 grid((unsigned)((Ni + 127) / 128), (unsigned)((No + 255) / 256), (unsigned)ns);
+        IADMM_ALLOW_LDS(gemm_tn_dma_kernel, kTnRingFloats * 4);
+        hipLaunchKernelGGL(gemm_tn_dma_kernel, grid, dim3(256), kTnRingFloats * 4, s, M, (int)Ni, (int)No,
+                           rows_per_split, X, Y, slab);
+      } else {
+        const dim3 grid((unsigned)((Ni + 127) / 128), (unsigned)((No + 127) / 128), (unsigned)ns);
+        hipLaunchKernelGGL(gemm_tn_kernel, grid, dim3(256), 0, s, M, (int)Ni, (int)No, rows_per_split, X, Y, slab);
+      }
     }
   }
   IADMM_CHECK_LAUNCH();

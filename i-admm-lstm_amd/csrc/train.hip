@@ -116,15 +116,20 @@ struct CellBwdArgs {
   float *inpart;                    // [njt][M][2]: sum over the tile's units of dP W^T
 };
 
+// Dynamic LDS: VEC: the LDS-DMA ring (cell_tile.h, kRingFloats); otherwise the register-staged
+// loop's two padded tiles.
+constexpr int kCellBwdLdsVec = kRingFloats * 4;
+constexpr int kCellBwdLdsScalar = (128 + kRows) * kLD * 4;
+
 template <bool VEC>
 __global__ __launch_bounds__(256, 2) void lstm_cell_bwd_kernel(CellBwdArgs a) {
-  __shared__ __attribute__((aligned(16))) float sA[128 * kLD];
-  __shared__ __attribute__((aligned(16))) float sB[kRows * kLD];
+  extern __shared__ __attribute__((aligned(16))) float dsm[];
   __shared__ __attribute__((aligned(16))) float sW[kWxF * kJT];
   __shared__ float swh[4][kJT];
   int jt, rt;
   cell_tile_of_block(a.njt, jt, rt);
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, jl = lane & 31, hf = lane >> 5;
+  const int tid = threadIdx.x, lane = tid & 63, jl = lane & 31, hf = lane >> 5;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int h = a.h;
   const int64_t M = a.M;
   const int64_t rbase = (int64_t)rt * kRows;
@@ -133,8 +138,14 @@ __global__ __launch_bounds__(256, 2) void lstm_cell_bwd_kernel(CellBwdArgs a) {
     sW[i] = a.Wx[(int64_t)(jt * kJT + jj) * kWxF + f];
   }
   floatx16 acc[4][2];
-  cell_mainloop<VEC>(a.H, M, h, a.nkc, a.Upk + (int64_t)jt * a.nkc * 128 * kBK, rbase, sA, sB, acc, tid,
-                     wave, jl, hf);
+  if constexpr (VEC) {
+    cell_mainloop_dma(a.H, M, h, a.nkc, a.Upk + (int64_t)jt * a.nkc * 128 * kBK, rbase, dsm, acc, tid, wave, jl,
+                      hf, [] {});
+    __syncthreads();  // sW visible (the DMA loop's barriers carry no LDS-write fence)
+  } else {
+    cell_mainloop<VEC>(a.H, M, h, a.nkc, a.Upk + (int64_t)jt * a.nkc * 128 * kBK, rbase, dsm, dsm + 128 * kLD,
+                       acc, tid, wave, jl, hf);
+  }
 
   float whp[16];
 #pragma unroll
@@ -458,8 +469,12 @@ extern "C" int iadmm_lstm_cell_bwd(int64_t M, int64_t h, const float* H, const f
   const bool vec = (h % 4 == 0) && aligned16(H) && aligned16(C) && aligned16(dC) && aligned16(dP) &&
                    (!dHn || aligned16(dHn)) && (!dCn || aligned16(dCn));
   const dim3 grid((unsigned)(nrt * njt));
-  if (vec) hipLaunchKernelGGL(lstm_cell_bwd_kernel<true>, grid, dim3(256), 0, (hipStream_t)stream, a);
-  else hipLaunchKernelGGL(lstm_cell_bwd_kernel<false>, grid, dim3(256), 0, (hipStream_t)stream, a);
+  if (vec) {
+    IADMM_ALLOW_LDS(lstm_cell_bwd_kernel<true>, kCellBwdLdsVec);
+    hipLaunchKernelGGL(lstm_cell_bwd_kernel<true>, grid, dim3(256), kCellBwdLdsVec, (hipStream_t)stream, a);
+  } else {
+    hipLaunchKernelGGL(lstm_cell_bwd_kernel<false>, grid, dim3(256), kCellBwdLdsScalar, (hipStream_t)stream, a);
+  }
   IADMM_CHECK_LAUNCH();
   return 0;
 }

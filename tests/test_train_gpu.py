@@ -77,7 +77,7 @@ def test_loss_grad_matches_autograd():
         assert rel_l2(mine.grad, ref.grad) < 1e-5
 
 
-@pytest.mark.parametrize("M,Ni,K", [(300, 40, 160), (1000, 130, 96), (257, 3, 50), (64, 800, 3200)])
+@pytest.mark.parametrize("M,Ni,K", [(300, 40, 160), (1000, 130, 96), (257, 3, 50), (64, 800, 3200), (513, 136, 100)])
 def test_gemm_nt_matches_fp64(M, Ni, K):
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
@@ -91,7 +91,7 @@ def test_gemm_nt_matches_fp64(M, Ni, K):
     assert rel_l2(acc, 2 * (X.double() @ W.double().T)) < tol
 
 
-@pytest.mark.parametrize("M,Ni,No", [(300, 40, 160), (5000, 130, 96), (4099, 3, 50)])
+@pytest.mark.parametrize("M,Ni,No", [(300, 40, 160), (5000, 130, 96), (4099, 3, 50), (5000, 136, 300), (2050, 800, 3200)])
 def test_gemm_tn_matches_fp64(M, Ni, No):
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
