@@ -133,9 +133,13 @@ __global__ __launch_bounds__(256, 2) void lstm_cell_bwd_kernel(CellBwdArgs a) {
   const int h = a.h;
   const int64_t M = a.M;
   const int64_t rbase = (int64_t)rt * kRows;
-  for (int i = tid; i < kWxF * kJT; i += 256) {
-    const int f = i / kJT, jj = i % kJT;
-    sW[i] = a.Wx[(int64_t)(jt * kJT + jj) * kWxF + f];
+  if constexpr (VEC) {
+    cell_fill_wpairs(a.Wx, jt, sW, tid, 256);  // pair-major, for the packed epilogue
+  } else {
+    for (int i = tid; i < kWxF * kJT; i += 256) {
+      const int f = i / kJT, jj = i % kJT;
+      sW[i] = a.Wx[(int64_t)(jt * kJT + jj) * kWxF + f];
+    }
   }
   floatx16 acc[4][2];
   if constexpr (VEC) {
@@ -150,6 +154,98 @@ __global__ __launch_bounds__(256, 2) void lstm_cell_bwd_kernel(CellBwdArgs a) {
   float whp[16];
 #pragma unroll
   for (int q = 0; q < 16; ++q) whp[q] = 0.f;
+  if constexpr (VEC) {
+    // Packed epilogue: unit pairs through v_pk_*_f32 (the forward's gate values bit for bit:
+    // same operations as cell_epi_compute).  h % 4 == 0: a lane's 4 units are all valid or not.
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+      const int64_t R = rbase + wave * 64 + r * 32 + jl;
+      const bool rok = R < M;
+      const float2v in0 = splat2(rok ? a.xv[R] : 0.f), in1 = splat2(rok ? a.g[R] : 0.f);
+      const float2v dqv = splat2(rok ? a.dq[R] : 0.f);
+      float2v din0 = splat2(0.f), din1 = splat2(0.f);
+#pragma unroll
+      for (int qq = 0; qq < 4; ++qq) {
+        __builtin_amdgcn_sched_barrier(0);
+        const int jj0 = 8 * qq + 4 * hf;
+        const int j0 = jt * kJT + jj0;
+        const int64_t o0 = R * h + j0;
+        const bool ok4 = rok && j0 < h;
+        // unconditional loads from a valid address, then a select (a conditional load here became
+        // a flat load through a pointer select with a private zero copy)
+        auto ld4z = [&](const float* base, bool ok) -> float4 {
+          const float4 t = *reinterpret_cast<const float4*>(ok ? base + o0 : a.C);
+          return ok ? t : make_float4(0.f, 0.f, 0.f, 0.f);
+        };
+        const float4 cin4 = ld4z(a.C, ok4);
+        const float4 dh4 = ld4z(a.dHn, ok4 && a.dHn);
+        const float4 dc4 = ld4z(a.dCn, ok4 && a.dCn);
+        float4 dC4, dP4[4];
+#pragma unroll
+        for (int pp = 0; pp < 2; ++pp) {
+          const float4* wp = reinterpret_cast<const float4*>(sW + ((jj0 >> 1) + pp) * 32);
+          float4 w4[7];
+#pragma unroll
+          for (int i = 0; i < 7; ++i) w4[i] = wp[i];
+          auto fld = [&](int f) -> float2v {
+            const float4& t = w4[f >> 1];
+            return (f & 1) ? float2v{t.z, t.w} : float2v{t.x, t.y};
+          };
+          auto half2 = [&](const float4& v) -> float2v { return pp ? float2v{v.z, v.w} : float2v{v.x, v.y}; };
+          const int q = qq * 4 + 2 * pp;
+          float2v pre[4];
+#pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            const float2v xw = in0 * fld(3 * g) + in1 * fld(3 * g + 1);
+            pre[g] = (xw + float2v{acc[g][r][q], acc[g][r][q + 1]}) + fld(3 * g + 2);
+          }
+          const float2v ig = sigmoid_cell2(pre[0]), fg = sigmoid_cell2(pre[1]), og = sigmoid_cell2(pre[2]);
+          const float2v ug = tanh_cell2(pre[3]);
+          const float2v cin = half2(cin4);
+          const float2v c2 = ig * ug + fg * cin;
+          const float2v tc = tanh_cell2(c2);
+          const float2v h2 = og * tc;
+          const float2v one = splat2(1.f);
+          const float2v dHt = half2(dh4) + dqv * fld(12);
+          const float2v dO = dHt * tc;
+          const float2v dCt = half2(dc4) + dHt * og * (one - tc * tc);
+          const float2v dI = dCt * ug, dU = dCt * ig, dF = dCt * cin;
+          const float2v dPi = dI * ig * (one - ig), dPf = dF * fg * (one - fg);
+          const float2v dPo = dO * og * (one - og), dPu = dU * (one - ug * ug);
+          const float2v dCo = dCt * fg;
+          if (pp == 0) {
+            dC4.x = dCo.x; dC4.y = dCo.y;
+            dP4[0].x = dPi.x; dP4[0].y = dPi.y; dP4[1].x = dPf.x; dP4[1].y = dPf.y;
+            dP4[2].x = dPo.x; dP4[2].y = dPo.y; dP4[3].x = dPu.x; dP4[3].y = dPu.y;
+          } else {
+            dC4.z = dCo.x; dC4.w = dCo.y;
+            dP4[0].z = dPi.x; dP4[0].w = dPi.y; dP4[1].z = dPf.x; dP4[1].w = dPf.y;
+            dP4[2].z = dPo.x; dP4[2].w = dPo.y; dP4[3].z = dPu.x; dP4[3].w = dPu.y;
+          }
+          if (ok4) {
+            const float2v wq = h2 * dqv;
+            whp[q] += wq.x;
+            whp[q + 1] += wq.y;
+            din0 += ((dPi * fld(0) + dPf * fld(3)) + dPo * fld(6)) + dPu * fld(9);
+            din1 += ((dPi * fld(1) + dPf * fld(4)) + dPo * fld(7)) + dPu * fld(10);
+          }
+        }
+        if (ok4) {
+          float* dp = a.dP + R * (int64_t)(4 * h) + j0;
+          *reinterpret_cast<float4*>(a.dC + o0) = dC4;
+#pragma unroll
+          for (int g = 0; g < 4; ++g) *reinterpret_cast<float4*>(dp + g * h) = dP4[g];
+        }
+      }
+      float d0 = din0.x + din0.y, d1 = din1.x + din1.y;
+      d0 += __shfl_xor(d0, 32, 64);
+      d1 += __shfl_xor(d1, 32, 64);
+      if (hf == 0 && rok) {
+        a.inpart[((int64_t)jt * M + R) * 2 + 0] = d0;
+        a.inpart[((int64_t)jt * M + R) * 2 + 1] = d1;
+      }
+    }
+  } else {
 #pragma unroll
   for (int r = 0; r < 2; ++r) {
     const int64_t R = rbase + wave * 64 + r * 32 + jl;
@@ -239,6 +335,7 @@ __global__ __launch_bounds__(256, 2) void lstm_cell_bwd_kernel(CellBwdArgs a) {
       a.inpart[((int64_t)jt * M + R) * 2 + 0] = din0;
       a.inpart[((int64_t)jt * M + R) * 2 + 1] = din1;
     }
+  }
   }
   // W_h gradient slab: sum of H' dq over this tile's 256 rows for its 32 units (fixed order)
 #pragma unroll
