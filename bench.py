@@ -106,8 +106,23 @@ def cpu_baseline(args, d, params):
                 final_primal=float(out["primal"].mean()), final_dual=float(out["dual"].mean()))
 
 
+def heartbeat(period_s=60.0):
+    """Print a progress line to stderr every ``period_s`` while a long step runs (config 4 takes
+    minutes per step; a silent process looks hung to a supervisor)."""
+    import threading
+    t0 = time.perf_counter()
+
+    def run():
+        while True:
+            time.sleep(period_s)
+            print(f"[bench] running, {time.perf_counter() - t0:.0f} s", file=sys.stderr, flush=True)
+
+    threading.Thread(target=run, daemon=True).start()
+
+
 def main():
     args = parse()
+    heartbeat()
     from iadmm import data, parallel, solver
     world, rank, local = parallel.env()
     local, backend = parallel.device_and_backend(local)
