@@ -124,7 +124,9 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(int64_t M, int Ni, int 
 // gemm_nt on the LDS-DMA main loop of the cell kernel (cell_tile.h mainloop_dma, A row-major):
 // K % 4 == 0 and 16-B aligned operands.  Workgroups remapped XCD-aware like the cell kernel so the
 // output tiles of one 256-row X panel run back to back on one XCD (panel reused from its L2).
-template <bool ACC>
+// A_PACKED: W given as iadmm_gemm_pack_a's [nit][ceil(K/32)][128][32] tiles (each DMA piece one
+// contiguous KiB) instead of row-major [Ni][K] (16 rows x 64 B per piece).
+template <bool ACC, bool A_PACKED = false>
 __global__ __launch_bounds__(256, 2) void gemm_nt_dma_kernel(int64_t M, int Ni, int K, const float* X,
                                                              const float* W, float* out) {
   extern __shared__ __attribute__((aligned(16))) float ring[];
@@ -137,8 +139,14 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_dma_kernel(int64_t M, int Ni, 
   const int i0 = it * 128;
   const int64_t r0 = rt * 256;
   floatx16 acc[4][2];
-  mainloop_dma<false>(W + (int64_t)i0 * K, Ni - i0, K, X + r0 * K, M - r0, K, K, ring, acc, tid, wave, jl, hf,
-                      [] {});
+  if constexpr (A_PACKED) {
+    const int64_t nkc32 = (K + kBK - 1) / kBK;
+    mainloop_dma<true>(W + (int64_t)it * nkc32 * 128 * kBK, 128, kBK, X + r0 * K, M - r0, K, K, ring, acc, tid,
+                       wave, jl, hf, [] {});
+  } else {
+    mainloop_dma<false>(W + (int64_t)i0 * K, Ni - i0, K, X + r0 * K, M - r0, K, K, ring, acc, tid, wave, jl, hf,
+                        [] {});
+  }
 #pragma unroll
   for (int r = 0; r < 2; ++r) {
     const int64_t R = r0 + wave * 64 + r * 32 + jl;
@@ -162,6 +170,21 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_dma_kernel(int64_t M, int Ni, 
             if (ib + e < Ni) o[e] = ACC ? o[e] + acc[g][r][4 * qq + e] : acc[g][r][4 * qq + e];
         }
       }
+  }
+}
+
+// Wpk[((it * nkc32 + kc) * 128 + row) * 32 + kk] = W[it*128 + row][kc*32 + kk]  (0 outside)
+__global__ void gemm_pack_a_kernel(int Ni, int K, int nit, int nkc32, const float* W, float* Wpk) {
+  const int64_t tot = (int64_t)nit * nkc32 * 128 * kBK;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < tot; i += (int64_t)gridDim.x * blockDim.x) {
+    const int kk = (int)(i % kBK);
+    int64_t t = i / kBK;
+    const int row = (int)(t % 128);
+    t /= 128;
+    const int kc = (int)(t % nkc32);
+    const int it = (int)(t / nkc32);
+    const int r = it * 128 + row, k = kc * kBK + kk;
+    Wpk[i] = (r < Ni && k < K) ? W[(int64_t)r * K + k] : 0.f;
   }
 }
 
@@ -290,32 +313,56 @@ __global__ __launch_bounds__(256, 2) void gemm_tn_dma_kernel(int64_t M, int Ni, 
       __builtin_amdgcn_raw_ptr_buffer_load_lds(yrs, (lds_void*)(sy + (wave * 4 + i) * 256), 16,
                                                yoff[i] == 0x80000000u ? yoff[i] : yoff[i] + oy, 0, 0, 0);
   };
-  auto mma_chunk = [&](int kc) {
+  // fragments of step ks (rows 2ks, 2ks+1) of chunk kc
+  auto frag = [&](int kc, int ks, float (&av)[4], float (&bv)[2]) {
     const float* sx = ring + (kc % 3) * (kTnStageX + kTnStageY);
     const float* sy = sx + kTnStageX;
+    const int kk = 2 * ks + hf;
 #pragma unroll
-    for (int ks = 0; ks < 8; ++ks) {
-      const int kk = 2 * ks + hf;
-      float av[4], bv[2];
+    for (int a = 0; a < 4; ++a) av[a] = sx[kk * 128 + a * 32 + jl];
 #pragma unroll
-      for (int a = 0; a < 4; ++a) av[a] = sx[kk * 128 + a * 32 + jl];
-#pragma unroll
-      for (int c = 0; c < 2; ++c) bv[c] = sy[kk * 256 + wave * 64 + c * 32 + jl];
-#pragma unroll
-      for (int a = 0; a < 4; ++a)
-#pragma unroll
-        for (int c = 0; c < 2; ++c)
-          acc[a][c] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[a], bv[c], acc[a][c], 0, 0, 0);
-    }
+    for (int c = 0; c < 2; ++c) bv[c] = sy[kk * 256 + wave * 64 + c * 32 + jl];
   };
+  auto mma = [&](const float (&av)[4], const float (&bv)[2]) {
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int c = 0; c < 2; ++c)
+        acc[a][c] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[a], bv[c], acc[a][c], 0, 0, 0);
+  };
+  // One barrier per chunk, after its first half: each wave has waited for its own pieces of chunk
+  // kc+1 (chunk kc+2 not yet issued), so after the barrier chunk kc+1 is readable and the stage of
+  // chunk kc-1 is free for chunk kc+2.  The first fragments of chunk kc+1 are read during the
+  // second half of chunk kc, so no chunk starts on an LDS-latency stall.
   issue(0);
   if (nk > 1) issue(1);
+  if (nk > 1) vm_wait<6>(); else vm_wait<0>();
+  __builtin_amdgcn_s_barrier();
+  float av0[4], bv0[2], av1[4], bv1[2];
+  frag(0, 0, av0, bv0);
   for (int kc = 0; kc < nk; ++kc) {
-    if (kc + 1 < nk) vm_wait<6>(); else vm_wait<0>();  // this wave's pieces of chunk kc
-    __builtin_amdgcn_s_barrier();                      // everyone's chunk kc landed; chunk kc-1 read
+#pragma unroll
+    for (int ks = 0; ks < 4; ks += 2) {
+      frag(kc, ks + 1, av1, bv1);
+      mma(av0, bv0);
+      frag(kc, ks + 2, av0, bv0);
+      mma(av1, bv1);
+    }
     __builtin_amdgcn_sched_barrier(0);
-    if (kc + 2 < nk) issue(kc + 2);
-    mma_chunk(kc);
+    if (kc + 1 < nk) {
+      vm_wait<0>();
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+      if (kc + 2 < nk) issue(kc + 2);
+    }
+#pragma unroll
+    for (int ks = 4; ks < 8; ks += 2) {
+      frag(kc, ks + 1, av1, bv1);
+      mma(av0, bv0);
+      if (ks + 2 < 8) frag(kc, ks + 2, av0, bv0);
+      else if (kc + 1 < nk) frag(kc + 1, 0, av0, bv0);
+      mma(av1, bv1);
+    }
     __builtin_amdgcn_sched_barrier(0);
   }
   float* S = slab + (int64_t)blockIdx.z * Ni * No;
@@ -421,6 +468,39 @@ extern "C" int iadmm_gemm_nt(int64_t M, int64_t Ni, int64_t K, const float* X, c
   } else {
     if (vec) hipLaunchKernelGGL((gemm_nt_kernel<false, true>), grid, dim3(256), 0, s, M, (int)Ni, (int)K, X, W, out);
     else hipLaunchKernelGGL((gemm_nt_kernel<false, false>), grid, dim3(256), 0, s, M, (int)Ni, (int)K, X, W, out);
+  }
+  IADMM_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int64_t iadmm_gemm_packed_a_floats(int64_t Ni, int64_t K) {
+  return ((Ni + 127) / 128) * ((K + kBK - 1) / kBK) * 128 * kBK;
+}
+
+extern "C" int iadmm_gemm_pack_a(int64_t Ni, int64_t K, const float* W, float* Wpk, void* stream) {
+  if (Ni <= 0 || K <= 0 || !W || !Wpk) return IADMM_E_ARG;
+  if (Ni > (1 << 20) || K > (1 << 20)) return IADMM_E_SIZE;
+  if (!aligned16(Wpk)) return IADMM_E_ALIGN;
+  hipLaunchKernelGGL(gemm_pack_a_kernel, dim3(2048), dim3(256), 0, (hipStream_t)stream, (int)Ni, (int)K,
+                     (int)((Ni + 127) / 128), (int)((K + kBK - 1) / kBK), W, Wpk);
+  IADMM_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int iadmm_gemm_nt_packed(int64_t M, int64_t Ni, int64_t K, const float* X, const float* Wpk,
+                                    float* out, int accumulate, void* stream) {
+  if (M <= 0 || Ni <= 0 || K <= 0 || !X || !Wpk || !out) return IADMM_E_ARG;
+  const int64_t nit = (Ni + 127) / 128, nrt = (M + 255) / 256;
+  if (nit * nrt > 0x7fffffffLL || Ni > (1 << 20) || K > (1 << 20) || K * 256 * 4 > 0x7fffffffLL) return IADMM_E_SIZE;
+  if (K % 4 || Ni % 4 || !aligned16(X) || !aligned16(Wpk) || !aligned16(out)) return IADMM_E_ALIGN;
+  const dim3 grid((unsigned)(nit * nrt));
+  hipStream_t s = (hipStream_t)stream;
+  if (accumulate) {
+    IADMM_ALLOW_LDS((gemm_nt_dma_kernel<true, true>), kRingFloats * 4);
+    hipLaunchKernelGGL((gemm_nt_dma_kernel<true, true>), grid, dim3(256), kRingFloats * 4, s, M, (int)Ni, (int)K, X, Wpk, out);
+  } else {
+    IADMM_ALLOW_LDS((gemm_nt_dma_kernel<false, true>), kRingFloats * 4);
+    hipLaunchKernelGGL((gemm_nt_dma_kernel<false, true>), grid, dim3(256), kRingFloats * 4, s, M, (int)Ni, (int)K, X, Wpk, out);
   }
   IADMM_CHECK_LAUNCH();
   return 0;

@@ -41,6 +41,9 @@ SIGNATURES = {
     "iadmm_kkt_rhs": (cint, [i64, i64, i64, i64, vp, vp, vp, vp, f32, vp, vp, vp, vp]),
     "iadmm_kkt_matvec": (cint, [i64, i64, i64, i64, vp, vp, vp, f32, vp, vp, cint, vp, vp]),
     "iadmm_gemm_nt": (cint, [i64, i64, i64, vp, vp, vp, cint, vp]),
+    "iadmm_gemm_packed_a_floats": (i64, [i64, i64]),
+    "iadmm_gemm_pack_a": (cint, [i64, i64, vp, vp, vp]),
+    "iadmm_gemm_nt_packed": (cint, [i64, i64, i64, vp, vp, vp, cint, vp]),
     "iadmm_gemm_tn_splits": (i64, [i64, i64]),
     "iadmm_gemm_tn": (cint, [i64, i64, i64, i64, vp, vp, vp, vp, cint, vp]),
     "iadmm_slab_reduce": (cint, [i64, i64, vp, vp, cint, vp]),

@@ -62,8 +62,8 @@ class IterationFn(torch.autograd.Function):
         Upk, Wx = packed.get({k: v.detach() for k, v in p.items()}, h)
         dC, dP, whslab, inpart = ops.lstm_cell_bwd(H, C, xv, g, Upk, Wx, dq, c(dHn), c(dCn))
         # 3. dH = dP U_cat^T ; [dU ; dW ; db] = [H, xv, g, 1]^T dP
-        Ucat = torch.cat([p["U_" + k].detach() for k in GATES], dim=1).contiguous()   # [h, 4h]
-        dH = ops.gemm_nt(dP, Ucat).reshape(H.shape)
+        Ucat_pk = packed.get_ucat_packed({k: v.detach() for k, v in p.items()}, h)     # [h, 4h], tiled
+        dH = ops.gemm_nt_packed(dP, Ucat_pk, h).reshape(H.shape)
         dUcat = ops.gemm_tn(H.reshape(M, h), dP)
         X3 = torch.stack([xv.reshape(M), g.reshape(M), torch.ones(M, device=x.device)], dim=1).contiguous()
         dW3 = ops.gemm_tn(X3, dP, rows_per_split=512)                                 # [3, 4h], streaming

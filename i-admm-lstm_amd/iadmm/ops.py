@@ -267,6 +267,22 @@ def gemm_nt(X, W, out=None, accumulate=False):
     return out
 
 
+def gemm_pack_a(W):
+    """W[Ni,K] -> the packed tile layout of gemm_nt_packed."""
+    Ni, K = W.shape
+    Wpk = empty(int(_abi.lib().iadmm_gemm_packed_a_floats(Ni, K)), like=W)
+    _abi.call("iadmm_gemm_pack_a", Ni, K, _p(W), _p(Wpk), _stream())
+    return Wpk
+
+
+def gemm_nt_packed(X, Wpk, Ni, out=None, accumulate=False):
+    """out[M,Ni] (+)= X[M,K] W[Ni,K]^T with W pre-packed by gemm_pack_a."""
+    M, K = X.shape
+    out = empty(M, Ni, like=X) if out is None else out
+    _abi.call("iadmm_gemm_nt_packed", M, Ni, K, _p(X), _p(Wpk), _p(out), int(bool(accumulate)), _stream())
+    return out
+
+
 def gemm_tn(X, Y, rows_per_split=4096, out=None, accumulate=False):
     """out[Ni,No] (+)= X[M,Ni]^T Y[M,No] (split over M, fixed-order reduction)."""
     M, Ni = X.shape

@@ -47,6 +47,17 @@ class PackedWeights:
             self._key = key
         return self.Upk, self.Wx
 
+    def get_ucat_packed(self, params, h):
+        """U_cat = [U_i U_f U_o U_u] ([h, 4h]) in gemm_nt_packed's tile layout: the A operand of
+        the backward's dH = dP U_cat^T (re-packed when a parameter changes)."""
+        key = self._version_key(params, h)
+        if key != getattr(self, "_key_ucat", None):
+            with torch.no_grad():
+                ucat = torch.cat([params["U_" + k].detach() for k in "ifou"], dim=1).contiguous()
+                self.Ucat_pk = ops.gemm_pack_a(ucat)
+            self._key_ucat = key
+        return self.Ucat_pk
+
     def get_f16x3(self, params, h):
         """Split weights of the optional f16x3 cell: (Upk16, wscale, Wx)."""
         _, Wx = self.get(params, h)

@@ -207,6 +207,14 @@ int iadmm_bmv(int64_t B, int64_t R, int64_t C, const float* M, const float* x, c
 int iadmm_gemm_nt(int64_t M, int64_t Ni, int64_t K, const float* X, const float* W, float* out,
                   int accumulate, void* stream);
 
+/* The same with W pre-packed by iadmm_gemm_pack_a into iadmm_gemm_packed_a_floats(Ni, K) floats
+ * ([ceil(Ni/128)][ceil(K/32)][128][32], zero-padded): every LDS-DMA piece of W is one contiguous
+ * KiB.  Requires K % 4 == 0, Ni % 4 == 0, 16-B aligned X, Wpk, out (IADMM_E_ALIGN otherwise). */
+int64_t iadmm_gemm_packed_a_floats(int64_t Ni, int64_t K);
+int iadmm_gemm_pack_a(int64_t Ni, int64_t K, const float* W, float* Wpk, void* stream);
+int iadmm_gemm_nt_packed(int64_t M, int64_t Ni, int64_t K, const float* X, const float* Wpk, float* out,
+                         int accumulate, void* stream);
+
 /* out[Ni,No] (+)= X[M,Ni]^T . Y[M,No], split over M in slices of rows_per_split (multiple of 32):
  * slab[iadmm_gemm_tn_splits(M, rows_per_split)][Ni][No] is caller-owned scratch.  fp32 MFMA for
  * Ni > 4 (dU_cat = H^T dP); Ni <= 4 (d[W_x; b] = [xv, g, 1]^T dP) streams Y once on the VALU. */

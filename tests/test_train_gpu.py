@@ -89,6 +89,12 @@ def test_gemm_nt_matches_fp64(M, Ni, K):
     assert rel_l2(out, X.double() @ W.double().T) < tol
     acc = ops.gemm_nt(X.cuda(), W.cuda(), out=out.clone(), accumulate=True)
     assert rel_l2(acc, 2 * (X.double() @ W.double().T)) < tol
+    if K % 4 == 0 and Ni % 4 == 0:  # the pre-packed A operand (same products, same order)
+        Wpk = ops.gemm_pack_a(W.cuda())
+        pk = ops.gemm_nt_packed(X.cuda(), Wpk, Ni)
+        assert torch.equal(pk, out)
+        pk = ops.gemm_nt_packed(X.cuda(), Wpk, Ni, out=pk, accumulate=True)
+        assert torch.equal(pk, acc)
 
 
 @pytest.mark.parametrize("M,Ni,No", [(300, 40, 160), (5000, 130, 96), (4099, 3, 50), (5000, 136, 300), (2050, 800, 3200)])

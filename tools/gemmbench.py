@@ -13,7 +13,8 @@ from iadmm import _abi  # noqa: E402
 
 def bind(path):
     lib = ctypes.CDLL(path)
-    for name in ("iadmm_gemm_nt", "iadmm_gemm_tn", "iadmm_gemm_tn_splits"):
+    for name in ("iadmm_gemm_nt", "iadmm_gemm_tn", "iadmm_gemm_tn_splits", "iadmm_gemm_pack_a",
+                 "iadmm_gemm_packed_a_floats", "iadmm_gemm_nt_packed"):
         f = getattr(lib, name)
         f.restype, f.argtypes = _abi.SIGNATURES[name]
     return lib
@@ -47,7 +48,14 @@ def main():
         name = os.path.basename(path)
         out_nt = torch.empty(M, h, device="cuda")
         t_nt = timeit(lambda: lib.iadmm_gemm_nt(M, h, 4 * h, p(dP), p(U), p(out_nt), 0, st))
-        rps = 4096
+        Wpk = torch.empty(int(lib.iadmm_gemm_packed_a_floats(h, 4 * h)), device="cuda")
+        lib.iadmm_gemm_pack_a(h, 4 * h, p(U), p(Wpk), st)
+        out_pk = torch.empty(M, h, device="cuda")
+        t_pk = timeit(lambda: lib.iadmm_gemm_nt_packed(M, h, 4 * h, p(dP), p(Wpk), p(out_pk), 0, st))
+        d_pk = float((out_pk - out_nt).abs().max() / out_nt.abs().max())
+        print(f"{name:20s} gemm_nt packed-A {t_pk:8.3f} ms {flop / t_pk / 1e9:7.1f} TF (vs row-major: diff {d_pk:.1e})",
+              flush=True)
+        rps = int(os.environ.get("GB_RPS", 4096))
         ns = lib.iadmm_gemm_tn_splits(M, rps)
         slab = torch.empty(ns, h, 4 * h, device="cuda")
         out_tn = torch.empty(h, 4 * h, device="cuda")
