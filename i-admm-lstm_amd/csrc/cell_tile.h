@@ -156,18 +156,25 @@ IADMM_DEV void vm_wait() {  // s_waitcnt vmcnt(N), other counters untouched (gfx
 // acc[g][r] += A[g*32 + .., k] . B[wave*64 + r*32 + .., k] over k < K, through the LDS ring.
 //   B: row-major panel (row stride ldb floats) starting at the workgroup's first row; rows past
 //      nb_valid and k past K read as zero (buffer range check / out-of-range offset).
-//   A: 128 rows.  A_PACKED: the fp32 32-deep packing of lstm_pack_kernel (Ubase = Upk +
-//      jt*nkc32*128*32, zero-padded, nkc32 = ceil(K/32)); otherwise row-major, row stride lda, rows
-//      past na_valid and k past K zero.
+//   A: NA*32 rows (NA = 4: the cell's 4 gates x 32 units; 5: 160-row GEMM tiles).  A_PACKED: the
+//      fp32 32-deep packing [ceil(K/32)][NA*32][32] (lstm_pack_kernel / gemm_pack_a; Abase = the
+//      tile's block, zero-padded); otherwise row-major, row stride lda, rows past na_valid and k
+//      past K zero.
 // before_last() runs once, just before the last chunk's MFMAs (e.g. to prefetch epilogue operands
 // behind them).
-template <bool A_PACKED, class BeforeLast>
+template <bool A_PACKED, int NA = 4, class BeforeLast>
 IADMM_DEV void mainloop_dma(const float* __restrict__ Abase, int na_valid, int lda,
                             const float* __restrict__ Bbase, int64_t nb_valid, int ldb, int K,
-                            float* ring, floatx16 (&acc)[4][2], int tid, int wave, int jl, int hf,
+                            float* ring, floatx16 (&acc)[NA][2], int tid, int wave, int jl, int hf,
                             BeforeLast&& before_last) {
+  static_assert(NA == 4 || NA == 5, "A tile = 4 or 5 blocks of 32 rows");
+  constexpr int AROWS = NA * 32;
+  constexpr int STA = AROWS * kBKd;                 // floats of the A part of a stage
+  constexpr int ST = STA + kStageB;                 // floats per stage
+  constexpr int NPA = NA * 2;                       // A pieces per chunk (16 rows each)
+  constexpr int APW = (NPA + 3) / 4;                // A pieces per wave (the last may be a dummy)
 #pragma unroll
-  for (int g = 0; g < 4; ++g)
+  for (int g = 0; g < NA; ++g)
 #pragma unroll
     for (int r = 0; r < 2; ++r)
 #pragma unroll
@@ -181,19 +188,22 @@ IADMM_DEV void mainloop_dma(const float* __restrict__ Abase, int na_valid, int l
       const_cast<float*>(Bbase), 0, (int)(nbv * ldb * 4), 0x00020000);
   const __amdgpu_buffer_rsrc_t urs = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<float*>(Abase), 0,
-      A_PACKED ? nkc32 * 128 * kBK * 4 : (na_valid < 128 ? na_valid : 128) * lda * 4, 0x00020000);
+      A_PACKED ? nkc32 * AROWS * kBK * 4 : (na_valid < AROWS ? na_valid : AROWS) * lda * 4, 0x00020000);
 
-  // Per-lane source offsets of this wave's pieces (piece = 16 LDS rows x 4 slots).
+  // Per-lane source offsets of this wave's pieces (piece = 16 LDS rows x 4 slots).  A piece p is
+  // issued by wave p % 4; a wave with fewer real pieces issues an out-of-range dummy into the
+  // scratch KiB after the ring (so every wave runs the same instruction stream).
   const int prow = lane >> 2, pslot = lane & 3;
-  unsigned aoff[2];
-  int ak4[2];
+  unsigned aoff[APW];
+  int ak4[APW];
   int bk4[4];
   unsigned boff[4];
 #pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int row = (wave * 2 + i) * 16 + prow;             // g*32 + jj
+  for (int i = 0; i < APW; ++i) {
+    const int p = wave + 4 * i;
+    const int row = p * 16 + prow;                          // g*32 + jj
     const int c = pslot ^ ((row >> 2) & 3);
-    ak4[i] = c * 4;
+    ak4[i] = p < NPA ? c * 4 : (1 << 30);                   // dummy: every k out of range
     aoff[i] = A_PACKED ? (unsigned)(row * kBK + c * 4) * 4u    // + kc32*16 KiB + half*64 B
                        : (unsigned)(row * lda + c * 4) * 4u;   // + kc*64 B
   }
@@ -206,17 +216,20 @@ IADMM_DEV void mainloop_dma(const float* __restrict__ Abase, int na_valid, int l
   }
   auto issue = [&](int kc) {
     const int st = kc % kStages;
-    float* sa = ring + st * (kStageA + kStageB);
-    float* sb = sa + kStageA;
+    float* sa = ring + st * ST;
+    float* sb = sa + STA;
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < APW; ++i) {
+      const int p = wave + 4 * i;
       unsigned o;
       if constexpr (A_PACKED) {
-        o = aoff[i] + (unsigned)((kc >> 1) * 128 * kBK + (kc & 1) * kBKd) * 4u;
+        o = (NPA % 4 == 0 || p < NPA) ? aoff[i] + (unsigned)((kc >> 1) * AROWS * kBK + (kc & 1) * kBKd) * 4u
+                                      : 0x80000000u;
       } else {
         o = (kc * kBKd + ak4[i] < K) ? aoff[i] + (unsigned)(kc * kBKd * 4) : 0x80000000u;
       }
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(urs, (lds_void*)(sa + (wave * 2 + i) * 256), 16, o, 0, 0, 0);
+      float* dst = (NPA % 4 == 0 || p < NPA) ? sa + p * 256 : ring + kStages * ST;  // dummy KiB
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(urs, (lds_void*)dst, 16, o, 0, 0, 0);
     }
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -229,28 +242,30 @@ IADMM_DEV void mainloop_dma(const float* __restrict__ Abase, int na_valid, int l
   const int aoffG[2] = {jl * kBKd + 4 * ((0 + hf) ^ sw), jl * kBKd + 4 * ((2 + hf) ^ sw)};
   const int boffG[2] = {(wave * 64 + jl) * kBKd + 4 * ((0 + hf) ^ sw),
                         (wave * 64 + jl) * kBKd + 4 * ((2 + hf) ^ sw)};
-  float4 fa0[4], fb0[2], fa1[4], fb1[2];
-  auto frag = [&](int kc, int G, float4 (&fa)[4], float4 (&fb)[2]) {
-    const float* sa = ring + (kc % kStages) * (kStageA + kStageB);
-    const float* sb = sa + kStageA;
+  float4 fa0[NA], fb0[2], fa1[NA], fb1[2];
+  auto frag = [&](int kc, int G, float4 (&fa)[NA], float4 (&fb)[2]) {
+    const float* sa = ring + (kc % kStages) * ST;
+    const float* sb = sa + STA;
 #pragma unroll
-    for (int g = 0; g < 4; ++g) fa[g] = *reinterpret_cast<const float4*>(sa + g * 32 * kBKd + aoffG[G]);
+    for (int g = 0; g < NA; ++g) fa[g] = *reinterpret_cast<const float4*>(sa + g * 32 * kBKd + aoffG[G]);
 #pragma unroll
     for (int r = 0; r < 2; ++r) fb[r] = *reinterpret_cast<const float4*>(sb + r * 32 * kBKd + boffG[G]);
   };
-  auto mma = [&](const float4 (&fa)[4], const float4 (&fb)[2]) {
+  auto mma = [&](const float4 (&fa)[NA], const float4 (&fb)[2]) {
 #pragma unroll
     for (int s = 0; s < 4; ++s)
 #pragma unroll
-      for (int g = 0; g < 4; ++g)
+      for (int g = 0; g < NA; ++g)
 #pragma unroll
         for (int r = 0; r < 2; ++r)
           acc[g][r] = __builtin_amdgcn_mfma_f32_32x32x2f32(get4(fa[g], s), get4(fb[r], s), acc[g][r], 0, 0, 0);
   };
+  constexpr int NRD = NA + 2;                       // fragment reads per half chunk
+  constexpr int NMF = 8 * NA;                       // MFMAs per half chunk
 
   issue(0);
   if (nk > 1) issue(1);
-  if (nk > 1) vm_wait<6>(); else vm_wait<0>();
+  if (nk > 1) vm_wait<APW + 4>(); else vm_wait<0>();
   __builtin_amdgcn_s_barrier();
   frag(0, 0, fa0, fb0);
   // The schedule is pinned with sched_group_barrier (the compiler otherwise sinks every fragment
@@ -262,11 +277,11 @@ IADMM_DEV void mainloop_dma(const float* __restrict__ Abase, int na_valid, int l
     frag(kc, 1, fa1, fb1);
     mma(fa0, fb0);
 #pragma unroll
-    for (int i = 0; i < 6; ++i) {
+    for (int i = 0; i < NRD; ++i) {
       __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // DS read
       __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
     }
-    __builtin_amdgcn_sched_group_barrier(0x008, 26, 0);
+    __builtin_amdgcn_sched_group_barrier(0x008, NMF - NRD, 0);
     __builtin_amdgcn_sched_barrier(0);
     vm_wait<0>();  // this wave's pieces of chunk kc+1 (chunk kc+2 is not issued yet)
     __builtin_amdgcn_s_barrier();
@@ -275,16 +290,16 @@ IADMM_DEV void mainloop_dma(const float* __restrict__ Abase, int na_valid, int l
     frag(kc + 1, 0, fa0, fb0);
     mma(fa1, fb1);
 #pragma unroll
-    for (int i = 0; i < 6; ++i) {
+    for (int i = 0; i < APW + 4; ++i) {
       __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);  // VMEM (LDS-DMA piece)
       __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
     }
 #pragma unroll
-    for (int i = 0; i < 6; ++i) {
+    for (int i = 0; i < NRD; ++i) {
       __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
       __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
     }
-    __builtin_amdgcn_sched_group_barrier(0x008, 20, 0);
+    __builtin_amdgcn_sched_group_barrier(0x008, NMF - NRD - APW - 4, 0);
     __builtin_amdgcn_sched_barrier(0);
   }
   frag(nk - 1, 1, fa1, fb1);  // last chunk, peeled
@@ -293,6 +308,10 @@ IADMM_DEV void mainloop_dma(const float* __restrict__ Abase, int na_valid, int l
   mma(fa0, fb0);
   mma(fa1, fb1);
 }
+
+// LDS floats of mainloop_dma<.., NA>'s ring (3 stages + the dummy-piece KiB when NA is odd).
+template <int NA>
+constexpr int dma_ring_floats() { return kStages * (NA * 32 * kBKd + kStageB) + ((NA * 2) % 4 ? 256 : 0); }
 
 // The cell's instance: A = the packed gate weights of hidden tile jt, B = the H panel of rows
 // [rbase, rbase + 256).

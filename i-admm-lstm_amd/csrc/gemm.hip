@@ -121,69 +121,93 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(int64_t M, int Ni, int 
   }
 }
 
-// gemm_nt on the LDS-DMA main loop of the cell kernel (cell_tile.h mainloop_dma, A row-major):
-// K % 4 == 0 and 16-B aligned operands.  Workgroups remapped XCD-aware like the cell kernel so the
-// output tiles of one 256-row X panel run back to back on one XCD (panel reused from its L2).
-// A_PACKED: W given as iadmm_gemm_pack_a's [nit][ceil(K/32)][128][32] tiles (each DMA piece one
+// gemm_nt on the LDS-DMA main loop of the cell kernel (cell_tile.h mainloop_dma): K % 4 == 0,
+// Ni % 4 == 0 and 16-B aligned operands.  Output tiles of NA*32 rows of W (NA = 4 or 5, whichever
+// pads Ni less: 800 = 5 x 160 wastes nothing where 128-row tiles compute 12 % padding) x 256 rows
+// of X.  Workgroups remapped XCD-aware like the cell kernel so the output tiles of one 256-row X
+// panel run back to back on one XCD (panel reused from its L2).
+// A_PACKED: W given as iadmm_gemm_pack_a's [nit][ceil(K/32)][NA*32][32] tiles (each DMA piece one
 // contiguous KiB) instead of row-major [Ni][K] (16 rows x 64 B per piece).
-template <bool ACC, bool A_PACKED = false>
+template <bool ACC, bool A_PACKED, int NA>
 __global__ __launch_bounds__(256, 2) void gemm_nt_dma_kernel(int64_t M, int Ni, int K, const float* X,
                                                              const float* W, float* out) {
   extern __shared__ __attribute__((aligned(16))) float ring[];
-  const int nit = (Ni + 127) / 128;
+  constexpr int TI = NA * 32;
+  const int nit = (Ni + TI - 1) / TI;
   int it, rti;
   cell_tile_of_block(nit, it, rti);
   const int64_t rt = rti;
   const int tid = threadIdx.x, lane = tid & 63, jl = lane & 31, hf = lane >> 5;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int i0 = it * 128;
+  const int i0 = it * TI;
   const int64_t r0 = rt * 256;
-  floatx16 acc[4][2];
+  floatx16 acc[NA][2];
   if constexpr (A_PACKED) {
     const int64_t nkc32 = (K + kBK - 1) / kBK;
-    mainloop_dma<true>(W + (int64_t)it * nkc32 * 128 * kBK, 128, kBK, X + r0 * K, M - r0, K, K, ring, acc, tid,
-                       wave, jl, hf, [] {});
+    mainloop_dma<true, NA>(W + (int64_t)it * nkc32 * TI * kBK, TI, kBK, X + r0 * K, M - r0, K, K, ring, acc, tid,
+                           wave, jl, hf, [] {});
   } else {
-    mainloop_dma<false>(W + (int64_t)i0 * K, Ni - i0, K, X + r0 * K, M - r0, K, K, ring, acc, tid, wave, jl, hf,
-                        [] {});
+    mainloop_dma<false, NA>(W + (int64_t)i0 * K, Ni - i0, K, X + r0 * K, M - r0, K, K, ring, acc, tid, wave, jl,
+                            hf, [] {});
   }
 #pragma unroll
   for (int r = 0; r < 2; ++r) {
     const int64_t R = r0 + wave * 64 + r * 32 + jl;
     if (R >= M) continue;
 #pragma unroll
-    for (int g = 0; g < 4; ++g)
+    for (int g = 0; g < NA; ++g)
 #pragma unroll
       for (int qq = 0; qq < 4; ++qq) {
         const int ib = i0 + g * 32 + 8 * qq + 4 * hf;
         float* o = out + R * Ni + ib;
-        if (ib + 3 < Ni) {
+        if (ib < Ni) {  // Ni % 4 == 0: the 4 outputs are all in range or all out
           float4 v = make_float4(acc[g][r][4 * qq], acc[g][r][4 * qq + 1], acc[g][r][4 * qq + 2], acc[g][r][4 * qq + 3]);
           if (ACC) {
             const float4 p = *reinterpret_cast<const float4*>(o);
             v.x += p.x; v.y += p.y; v.z += p.z; v.w += p.w;
           }
           *reinterpret_cast<float4*>(o) = v;
-        } else {
-#pragma unroll
-          for (int e = 0; e < 4; ++e)
-            if (ib + e < Ni) o[e] = ACC ? o[e] + acc[g][r][4 * qq + e] : acc[g][r][4 * qq + e];
         }
       }
   }
 }
 
-// Wpk[((it * nkc32 + kc) * 128 + row) * 32 + kk] = W[it*128 + row][kc*32 + kk]  (0 outside)
-__global__ void gemm_pack_a_kernel(int Ni, int K, int nit, int nkc32, const float* W, float* Wpk) {
-  const int64_t tot = (int64_t)nit * nkc32 * 128 * kBK;
+// Output-tile height of the DMA gemm_nt: 160 rows when that pads Ni less than 128 rows would.
+inline int gemm_nt_tile(int64_t Ni) {
+  const int64_t w128 = (Ni + 127) / 128 * 128 - Ni, w160 = (Ni + 159) / 160 * 160 - Ni;
+  return w160 < w128 ? 160 : 128;
+}
+
+template <bool ACC, bool A_PACKED>
+int launch_gemm_nt_dma(int64_t M, int64_t Ni, int64_t K, const float* X, const float* W, float* out, hipStream_t s) {
+  const int ti = gemm_nt_tile(Ni);
+  const int64_t nit = (Ni + ti - 1) / ti, nrt = (M + 255) / 256;
+  if (nit * nrt > 0x7fffffffLL) return IADMM_E_SIZE;
+  const dim3 grid((unsigned)(nit * nrt));
+  if (ti == 160) {
+    constexpr int lds = dma_ring_floats<5>() * 4;
+    IADMM_ALLOW_LDS((gemm_nt_dma_kernel<ACC, A_PACKED, 5>), lds);
+    hipLaunchKernelGGL((gemm_nt_dma_kernel<ACC, A_PACKED, 5>), grid, dim3(256), lds, s, M, (int)Ni, (int)K, X, W, out);
+  } else {
+    constexpr int lds = dma_ring_floats<4>() * 4;
+    IADMM_ALLOW_LDS((gemm_nt_dma_kernel<ACC, A_PACKED, 4>), lds);
+    hipLaunchKernelGGL((gemm_nt_dma_kernel<ACC, A_PACKED, 4>), grid, dim3(256), lds, s, M, (int)Ni, (int)K, X, W, out);
+  }
+  IADMM_CHECK_LAUNCH();
+  return 0;
+}
+
+// Wpk[((it * nkc32 + kc) * TI + row) * 32 + kk] = W[it*TI + row][kc*32 + kk]  (0 outside)
+__global__ void gemm_pack_a_kernel(int Ni, int K, int TI, int nit, int nkc32, const float* W, float* Wpk) {
+  const int64_t tot = (int64_t)nit * nkc32 * TI * kBK;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < tot; i += (int64_t)gridDim.x * blockDim.x) {
     const int kk = (int)(i % kBK);
     int64_t t = i / kBK;
-    const int row = (int)(t % 128);
-    t /= 128;
+    const int row = (int)(t % TI);
+    t /= TI;
     const int kc = (int)(t % nkc32);
     const int it = (int)(t / nkc32);
-    const int r = it * 128 + row, k = kc * kBK + kk;
+    const int r = it * TI + row, k = kc * kBK + kk;
     Wpk[i] = (r < Ni && k < K) ? W[(int64_t)r * K + k] : 0.f;
   }
 }
@@ -254,30 +278,34 @@ __global__ __launch_bounds__(256, 2) void gemm_tn_kernel(int64_t M, int Ni, int 
 }
 
 // gemm_tn on an LDS-DMA ring (the cell kernel's pipeline with the contraction over rows):
-// workgroup = 128 (i) x 256 (o) outputs of one row split, wave = 128 (i) x 64 (o) = 4 x 2
-// accumulators of v_mfma_f32_32x32x2_f32.  Per 16-row chunk each wave DMAs 2 pieces of the X
-// panel (2 rows x 128 columns each) and 4 of the Y panel (1 row x 256 columns each) into a 3-stage
-// ring, row-major as in HBM (lane-linear DMA image); fragments are ds_read_b32 of 32 consecutive
-// columns of one row per half-wave (conflict-free without a swizzle).  Rows past the split and
-// columns past Ni / No read as zero (buffer range / out-of-range offsets).  One barrier per chunk;
-// the chunk kc+2 DMA is issued after it, into the stage chunk kc-1 used.  Requires
-// Ni % 4 == No % 4 == 0 and 16-B aligned X, Y.
-constexpr int kTnStageX = 16 * 128, kTnStageY = 16 * 256;
-constexpr int kTnRingFloats = 3 * (kTnStageX + kTnStageY);
+// workgroup = NA*32 (i) x 256 (o) outputs of one row split (NA = 4 or 5 as for gemm_nt: 160-wide
+// i tiles cover Ni = 800 exactly), wave = NA*32 (i) x 64 (o) = NA x 2 accumulators of
+// v_mfma_f32_32x32x2_f32.  Per 16-row chunk the workgroup DMAs the X panel (16 rows x NA*32
+// columns, lane-linear KiB pieces) and 16 Y pieces (1 row x 256 columns each) into a 3-stage ring,
+// row-major as in HBM; fragments are ds_read_b32 of 32 consecutive columns of one row per
+// half-wave (conflict-free without a swizzle).  Rows past the split and columns past Ni / No read
+// as zero (buffer range / out-of-range offsets).  One barrier per chunk; the chunk kc+2 DMA is
+// issued after it, into the stage chunk kc-1 used.  Requires Ni % 4 == No % 4 == 0 and 16-B
+// aligned X, Y.
+template <int NA>
+constexpr int tn_ring_floats() {
+  return 3 * (16 * NA * 32 + 16 * 256) + ((NA * 2) % 4 ? 256 : 0);  // + the dummy-piece KiB
+}
 
-__global__ __launch_bounds__(256, 2) void gemm_tn_dma_kernel(int64_t M, int Ni, int No, int64_t rows_per_split,
-                                                             const float* X, const float* Y, float* slab) {
-  extern __shared__ __attribute__((aligned(16))) float ring[];
+template <int NA>
+IADMM_DEV void gemm_tn_dma_body(int64_t M, int Ni, int No, int64_t rows_per_split, const float* X, const float* Y,
+                                float* slab, float* ring) {
+  constexpr int TI = NA * 32, SX = 16 * TI, SY = 16 * 256, NPX = NA * 2, XPW = (NPX + 3) / 4;
   const int tid = threadIdx.x, lane = tid & 63, jl = lane & 31, hf = lane >> 5;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int i0 = blockIdx.x * 128, o0 = blockIdx.y * 256;
+  const int i0 = blockIdx.x * TI, o0 = blockIdx.y * 256;
   const int64_t rbeg = (int64_t)blockIdx.z * rows_per_split;
   const int64_t rend = min(M, rbeg + rows_per_split);
   const int nrows = (int)(rend - rbeg);
   const int nk = (nrows + 15) / 16;
-  floatx16 acc[4][2];
+  floatx16 acc[NA][2];
 #pragma unroll
-  for (int a = 0; a < 4; ++a)
+  for (int a = 0; a < NA; ++a)
 #pragma unroll
     for (int c = 0; c < 2; ++c)
 #pragma unroll
@@ -287,13 +315,15 @@ __global__ __launch_bounds__(256, 2) void gemm_tn_dma_kernel(int64_t M, int Ni, 
       const_cast<float*>(X + rbeg * Ni), 0, (int)((int64_t)nrows * Ni * 4), 0x00020000);
   const __amdgpu_buffer_rsrc_t yrs = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<float*>(Y + rbeg * No), 0, (int)((int64_t)nrows * No * 4), 0x00020000);
-  // X piece p (1 KiB) = stage rows 2p, 2p+1 (lane >> 5), columns i0 + 4*(lane & 31) .. +4
-  // Y piece q (1 KiB) = stage row q, columns o0 + 4*lane .. +4
-  unsigned xoff[2], yoff[4];
+  // X piece p (wave p % 4) = stage floats [256p, 256p + 256): lane -> float 256p + 4*lane, i.e.
+  // row / column of the [16][TI] image; a wave with no piece left issues an out-of-range dummy
+  // into the KiB after the ring.  Y piece q = stage row q, columns o0 + 4*lane .. +4.
+  unsigned xoff[XPW], yoff[4];
 #pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int row = (wave * 2 + i) * 2 + (lane >> 5), col = i0 + (lane & 31) * 4;
-    xoff[i] = (col < Ni) ? (unsigned)(row * Ni + col) * 4u : 0x80000000u;
+  for (int i = 0; i < XPW; ++i) {
+    const int p = wave + 4 * i, idx = 256 * p + 4 * lane;
+    const int row = idx / TI, col = i0 + idx % TI;
+    xoff[i] = (p < NPX && col < Ni) ? (unsigned)(row * Ni + col) * 4u : 0x80000000u;
   }
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
@@ -301,31 +331,34 @@ __global__ __launch_bounds__(256, 2) void gemm_tn_dma_kernel(int64_t M, int Ni, 
     yoff[i] = (col < No) ? (unsigned)(row * No + col) * 4u : 0x80000000u;
   }
   auto issue = [&](int kc) {
-    float* sx = ring + (kc % 3) * (kTnStageX + kTnStageY);
-    float* sy = sx + kTnStageX;
+    float* sx = ring + (kc % 3) * (SX + SY);
+    float* sy = sx + SX;
     const unsigned ox = (unsigned)(kc * 16 * Ni) * 4u, oy = (unsigned)(kc * 16 * No) * 4u;
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(xrs, (lds_void*)(sx + (wave * 2 + i) * 256), 16,
+    for (int i = 0; i < XPW; ++i) {
+      const int p = wave + 4 * i;
+      float* dst = (NPX % 4 == 0 || p < NPX) ? sx + p * 256 : ring + 3 * (SX + SY);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(xrs, (lds_void*)dst, 16,
                                                xoff[i] == 0x80000000u ? xoff[i] : xoff[i] + ox, 0, 0, 0);
+    }
 #pragma unroll
     for (int i = 0; i < 4; ++i)
       __builtin_amdgcn_raw_ptr_buffer_load_lds(yrs, (lds_void*)(sy + (wave * 4 + i) * 256), 16,
                                                yoff[i] == 0x80000000u ? yoff[i] : yoff[i] + oy, 0, 0, 0);
   };
   // fragments of step ks (rows 2ks, 2ks+1) of chunk kc
-  auto frag = [&](int kc, int ks, float (&av)[4], float (&bv)[2]) {
-    const float* sx = ring + (kc % 3) * (kTnStageX + kTnStageY);
-    const float* sy = sx + kTnStageX;
+  auto frag = [&](int kc, int ks, float (&av)[NA], float (&bv)[2]) {
+    const float* sx = ring + (kc % 3) * (SX + SY);
+    const float* sy = sx + SX;
     const int kk = 2 * ks + hf;
 #pragma unroll
-    for (int a = 0; a < 4; ++a) av[a] = sx[kk * 128 + a * 32 + jl];
+    for (int a = 0; a < NA; ++a) av[a] = sx[kk * TI + a * 32 + jl];
 #pragma unroll
     for (int c = 0; c < 2; ++c) bv[c] = sy[kk * 256 + wave * 64 + c * 32 + jl];
   };
-  auto mma = [&](const float (&av)[4], const float (&bv)[2]) {
+  auto mma = [&](const float (&av)[NA], const float (&bv)[2]) {
 #pragma unroll
-    for (int a = 0; a < 4; ++a)
+    for (int a = 0; a < NA; ++a)
 #pragma unroll
       for (int c = 0; c < 2; ++c)
         acc[a][c] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[a], bv[c], acc[a][c], 0, 0, 0);
@@ -336,9 +369,9 @@ __global__ __launch_bounds__(256, 2) void gemm_tn_dma_kernel(int64_t M, int Ni, 
   // second half of chunk kc, so no chunk starts on an LDS-latency stall.
   issue(0);
   if (nk > 1) issue(1);
-  if (nk > 1) vm_wait<6>(); else vm_wait<0>();
+  if (nk > 1) vm_wait<XPW + 4>(); else vm_wait<0>();
   __builtin_amdgcn_s_barrier();
-  float av0[4], bv0[2], av1[4], bv1[2];
+  float av0[NA], bv0[2], av1[NA], bv1[2];
   frag(0, 0, av0, bv0);
   for (int kc = 0; kc < nk; ++kc) {
 #pragma unroll
@@ -367,7 +400,7 @@ __global__ __launch_bounds__(256, 2) void gemm_tn_dma_kernel(int64_t M, int Ni, 
   }
   float* S = slab + (int64_t)blockIdx.z * Ni * No;
 #pragma unroll
-  for (int a = 0; a < 4; ++a)
+  for (int a = 0; a < NA; ++a)
 #pragma unroll
     for (int c = 0; c < 2; ++c)
 #pragma unroll
@@ -376,6 +409,19 @@ __global__ __launch_bounds__(256, 2) void gemm_tn_dma_kernel(int64_t M, int Ni, 
         const int o = o0 + wave * 64 + c * 32 + jl;
         if (i < Ni && o < No) S[(int64_t)i * No + o] = acc[a][c][q];
       }
+}
+
+// (two plain kernels: a __global__ template instantiated from the extern "C" launcher got no host
+// stub from this hipcc)
+__global__ __launch_bounds__(256, 2) void gemm_tn_dma4_kernel(int64_t M, int Ni, int No, int64_t rps, const float* X,
+                                                              const float* Y, float* slab) {
+  extern __shared__ __attribute__((aligned(16))) float ring[];
+  gemm_tn_dma_body<4>(M, Ni, No, rps, X, Y, slab, ring);
+}
+__global__ __launch_bounds__(256, 2) void gemm_tn_dma5_kernel(int64_t M, int Ni, int No, int64_t rps, const float* X,
+                                                              const float* Y, float* slab) {
+  extern __shared__ __attribute__((aligned(16))) float ring[];
+  gemm_tn_dma_body<5>(M, Ni, No, rps, X, Y, slab, ring);
 }
 
 // Skinny X^T Y (Ni <= 4, e.g. the [xv, g, 1]^T dP bias/input-weight gradient): a streaming
@@ -455,13 +501,8 @@ extern "C" int iadmm_gemm_nt(int64_t M, int64_t Ni, int64_t K, const float* X, c
   hipStream_t s = (hipStream_t)stream;
   const bool dma = vec && K * 256 * 4 <= 0x7fffffffLL;  // the DMA kernel's epilogue stores float4 rows
   if (dma) {
-    if (accumulate) {
-      IADMM_ALLOW_LDS(gemm_nt_dma_kernel<true>, kRingFloats * 4);
-      hipLaunchKernelGGL((gemm_nt_dma_kernel<true>), grid, dim3(256), kRingFloats * 4, s, M, (int)Ni, (int)K, X, W, out);
-    } else {
-      IADMM_ALLOW_LDS(gemm_nt_dma_kernel<false>, kRingFloats * 4);
-      hipLaunchKernelGGL((gemm_nt_dma_kernel<false>), grid, dim3(256), kRingFloats * 4, s, M, (int)Ni, (int)K, X, W, out);
-    }
+    return accumulate ? launch_gemm_nt_dma<true, false>(M, Ni, K, X, W, out, s)
+                      : launch_gemm_nt_dma<false, false>(M, Ni, K, X, W, out, s);
   } else if (accumulate) {
     if (vec) hipLaunchKernelGGL((gemm_nt_kernel<true, true>), grid, dim3(256), 0, s, M, (int)Ni, (int)K, X, W, out);
     else hipLaunchKernelGGL((gemm_nt_kernel<true, false>), grid, dim3(256), 0, s, M, (int)Ni, (int)K, X, W, out);
@@ -474,15 +515,17 @@ extern "C" int iadmm_gemm_nt(int64_t M, int64_t Ni, int64_t K, const float* X, c
 }
 
 extern "C" int64_t iadmm_gemm_packed_a_floats(int64_t Ni, int64_t K) {
-  return ((Ni + 127) / 128) * ((K + kBK - 1) / kBK) * 128 * kBK;
+  const int ti = gemm_nt_tile(Ni);
+  return ((Ni + ti - 1) / ti) * ((K + kBK - 1) / kBK) * ti * kBK;
 }
 
 extern "C" int iadmm_gemm_pack_a(int64_t Ni, int64_t K, const float* W, float* Wpk, void* stream) {
   if (Ni <= 0 || K <= 0 || !W || !Wpk) return IADMM_E_ARG;
   if (Ni > (1 << 20) || K > (1 << 20)) return IADMM_E_SIZE;
   if (!aligned16(Wpk)) return IADMM_E_ALIGN;
-  hipLaunchKernelGGL(gemm_pack_a_kernel, dim3(2048), dim3(256), 0, (hipStream_t)stream, (int)Ni, (int)K,
-                     (int)((Ni + 127) / 128), (int)((K + kBK - 1) / kBK), W, Wpk);
+  const int ti = gemm_nt_tile(Ni);
+  hipLaunchKernelGGL(gemm_pack_a_kernel, dim3(2048), dim3(256), 0, (hipStream_t)stream, (int)Ni, (int)K, ti,
+                     (int)((Ni + ti - 1) / ti), (int)((K + kBK - 1) / kBK), W, Wpk);
   IADMM_CHECK_LAUNCH();
   return 0;
 }
@@ -490,20 +533,11 @@ extern "C" int iadmm_gemm_pack_a(int64_t Ni, int64_t K, const float* W, float* W
 extern "C" int iadmm_gemm_nt_packed(int64_t M, int64_t Ni, int64_t K, const float* X, const float* Wpk,
                                     float* out, int accumulate, void* stream) {
   if (M <= 0 || Ni <= 0 || K <= 0 || !X || !Wpk || !out) return IADMM_E_ARG;
-  const int64_t nit = (Ni + 127) / 128, nrt = (M + 255) / 256;
-  if (nit * nrt > 0x7fffffffLL || Ni > (1 << 20) || K > (1 << 20) || K * 256 * 4 > 0x7fffffffLL) return IADMM_E_SIZE;
+  if (Ni > (1 << 20) || K > (1 << 20) || K * 256 * 4 > 0x7fffffffLL) return IADMM_E_SIZE;
   if (K % 4 || Ni % 4 || !aligned16(X) || !aligned16(Wpk) || !aligned16(out)) return IADMM_E_ALIGN;
-  const dim3 grid((unsigned)(nit * nrt));
   hipStream_t s = (hipStream_t)stream;
-  if (accumulate) {
-    IADMM_ALLOW_LDS((gemm_nt_dma_kernel<true, true>), kRingFloats * 4);
-    hipLaunchKernelGGL((gemm_nt_dma_kernel<true, true>), grid, dim3(256), kRingFloats * 4, s, M, (int)Ni, (int)K, X, Wpk, out);
-  } else {
-    IADMM_ALLOW_LDS((gemm_nt_dma_kernel<false, true>), kRingFloats * 4);
-    hipLaunchKernelGGL((gemm_nt_dma_kernel<false, true>), grid, dim3(256), kRingFloats * 4, s, M, (int)Ni, (int)K, X, Wpk, out);
-  }
-  IADMM_CHECK_LAUNCH();
-  return 0;
+  return accumulate ? launch_gemm_nt_dma<true, true>(M, Ni, K, X, Wpk, out, s)
+                    : launch_gemm_nt_dma<false, true>(M, Ni, K, X, Wpk, out, s);
 }
 
 extern "C" int64_t iadmm_gemm_tn_splits(int64_t M, int64_t rows_per_split) {
@@ -525,11 +559,18 @@ extern "C" int iadmm_gemm_tn(int64_t M, int64_t Ni, int64_t No, int64_t rows_per
     default: {
       const bool dma = Ni % 4 == 0 && No % 4 == 0 && aligned16(X) && aligned16(Y) && rows_per_split % 16 == 0 &&
                        rows_per_split * (Ni > No ? Ni : No) * 4 <= 0x7fffffffLL;
-      if (dma) {
+      if (dma && gemm_nt_tile(Ni) == 160) {
+        const dim3 grid((unsigned)((Ni + 159) / 160), (unsigned)((No + 255) / 256), (unsigned)ns);
+        constexpr int lds = tn_ring_floats<5>() * 4;
+        IADMM_ALLOW_LDS(gemm_tn_dma5_kernel, lds);
+        hipLaunchKernelGGL(gemm_tn_dma5_kernel, grid, dim3(256), lds, s, M, (int)Ni, (int)No, rows_per_split, X, Y,
+                           slab);
+      } else if (dma) {
         const dim3 grid((unsigned)((Ni + 127) / 128), (unsigned)((No + 255) / 256), (unsigned)ns);
-        IADMM_ALLOW_LDS(gemm_tn_dma_kernel, kTnRingFloats * 4);
-        hipLaunchKernelGGL(gemm_tn_dma_kernel, grid, dim3(256), kTnRingFloats * 4, s, M, (int)Ni, (int)No,
-                           rows_per_split, X, Y, slab);
+        constexpr int lds = tn_ring_floats<4>() * 4;
+        IADMM_ALLOW_LDS(gemm_tn_dma4_kernel, lds);
+        hipLaunchKernelGGL(gemm_tn_dma4_kernel, grid, dim3(256), lds, s, M, (int)Ni, (int)No, rows_per_split, X, Y,
+                           slab);
       } else {
         const dim3 grid((unsigned)((Ni + 127) / 128), (unsigned)((No + 127) / 128), (unsigned)ns);
         hipLaunchKernelGGL(gemm_tn_kernel, grid, dim3(256), 0, s, M, (int)Ni, (int)No, rows_per_split, X, Y, slab);
