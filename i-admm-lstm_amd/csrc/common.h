@@ -48,7 +48,11 @@ constexpr float kLN2 = 0.693147181f;
 constexpr float kTh4 = -0.0057040372917676625f, kTh3 = 0.020637863933015994f, kTh2 = -0.05373916009365762f,
                 kTh1 = 0.13331431844163766f, kTh0 = -0.3333328129024227f;
 
+// y is clamped to [-87, 88] first (v_med3): e^y stays finite, so the fma correction never meets
+// inf (inf * negative + inf = NaN) and +-inf inputs give sigmoid 0 / 1 like torch; beyond the clamp
+// the sigmoid differs from the exact value by < 1e-38.
 IADMM_DEV float exp_cell(float y) {
+  y = __builtin_amdgcn_fmed3f(y, -87.0f, 88.0f);
   const float th = y * kL2E;
   float tl = fmaf(y, kL2E, -th);
   tl = fmaf(y, kL2E_LO, tl);
@@ -72,6 +76,7 @@ IADMM_DEV float tanh_cell(float x) {
 IADMM_DEV float2v fma2(float2v a, float2v b, float2v c) { return __builtin_elementwise_fma(a, b, c); }
 IADMM_DEV float2v splat2(float v) { return float2v{v, v}; }
 IADMM_DEV float2v exp_cell2(float2v y) {
+  y = float2v{__builtin_amdgcn_fmed3f(y.x, -87.0f, 88.0f), __builtin_amdgcn_fmed3f(y.y, -87.0f, 88.0f)};
   const float2v th = y * splat2(kL2E);
   float2v tl = fma2(y, splat2(kL2E), -th);
   tl = fma2(y, splat2(kL2E_LO), tl);

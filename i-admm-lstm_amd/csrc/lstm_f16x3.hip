@@ -106,10 +106,7 @@ __global__ __launch_bounds__(256, 2) void cell_f16x3_kernel(CellF16x3Args a) {
   const int64_t M = a.M, MH = a.M * (int64_t)a.h;
   const int64_t rbase = (int64_t)rt * kRows;
 
-  for (int i = tid; i < kWxF * kJT; i += 256) {
-    const int f = i / kJT, jj = i % kJT;
-    sW[i] = a.Wx[(int64_t)(jt * kJT + jj) * kWxF + f];
-  }
+  cell_fill_wpairs(a.Wx, jt, sW, tid, 256);  // pair-major, for the packed epilogue
 
   floatx16 acc[4][2];
 #pragma unroll
@@ -187,45 +184,57 @@ __global__ __launch_bounds__(256, 2) void cell_f16x3_kernel(CellF16x3Args a) {
     if constexpr (PRIO == 1) __builtin_amdgcn_s_setprio(0);
   }
 
-  // ---- epilogue (as cell_fwd_kernel) + split planes of H'
+  // ---- epilogue: the fp32 kernel's packed cell math (cell_epi_compute) on the 2^-s-rescaled
+  // accumulators, + the split planes of H'
   const float inv = a.wscale[1];
 #pragma unroll
   for (int r = 0; r < 2; ++r) {
     const int64_t R = rbase + wave * 64 + r * 32 + jl;
     const bool rok = R < M;
-    const float in0 = rok ? a.xv[R] : 0.f;
-    const float in1 = rok ? a.g[R] : 0.f;
-    float gsum = 0.f;
+    const float2v in0 = splat2(rok ? a.xv[R] : 0.f), in1 = splat2(rok ? a.g[R] : 0.f);
+    float2v gs = splat2(0.f);
 #pragma unroll
     for (int qq = 0; qq < 4; ++qq) {
+      __builtin_amdgcn_sched_barrier(0);
       const int jj0 = 8 * qq + 4 * hf;
       const int j0 = jt * kJT + jj0;
       const bool ok4 = rok && j0 < h;  // h % 8 == 0: the 4 units are all in range or all out
-      const float4 cold = ok4 ? *reinterpret_cast<const float4*>(a.C + R * h + j0) : make_float4(0.f, 0.f, 0.f, 0.f);
-      float4 wv[13];
-#pragma unroll
-      for (int f = 0; f < 13; ++f) wv[f] = *reinterpret_cast<const float4*>(&sW[f * kJT + jj0]);
+      const float4 t4 = *reinterpret_cast<const float4*>(a.C + (ok4 ? R * h + j0 : 0));
+      const float4 cold = ok4 ? t4 : make_float4(0.f, 0.f, 0.f, 0.f);
       float4 cnew, hnew;
       half4 hhi, hlo;
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int q = qq * 4 + e;
-        float pre[4];
+      for (int pp = 0; pp < 2; ++pp) {
+        const float4* wp = reinterpret_cast<const float4*>(sW + ((jj0 >> 1) + pp) * 32);
+        float4 w4[7];
+#pragma unroll
+        for (int i = 0; i < 7; ++i) w4[i] = wp[i];
+        auto fld = [&](int f) -> float2v {
+          const float4& t = w4[f >> 1];
+          return (f & 1) ? float2v{t.z, t.w} : float2v{t.x, t.y};
+        };
+        const int q = qq * 4 + 2 * pp;
+        float2v pre[4];
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
-          const float xw = in0 * get4(wv[3 * g], e) + in1 * get4(wv[3 * g + 1], e);
-          pre[g] = (xw + acc[g][r][q] * inv) + get4(wv[3 * g + 2], e);
+          const float2v xw = in0 * fld(3 * g) + in1 * fld(3 * g + 1);
+          pre[g] = (xw + float2v{acc[g][r][q], acc[g][r][q + 1]} * splat2(inv)) + fld(3 * g + 2);
         }
-        const float ig = sigmoid_cell(pre[0]), fg = sigmoid_cell(pre[1]), og = sigmoid_cell(pre[2]);
-        const float ug = tanh_cell(pre[3]);
-        const float c2 = ig * ug + fg * get4(cold, e);
-        const float h2 = og * tanh_cell(c2);
-        set4(cnew, e, c2);
-        set4(hnew, e, h2);
-        const _Float16 hi = (_Float16)h2;
-        hhi[e] = hi;
-        hlo[e] = (_Float16)(h2 - (float)hi);
-        gsum = fmaf(h2, get4(wv[12], e), gsum);
+        const float2v ig = sigmoid_cell2(pre[0]), fg = sigmoid_cell2(pre[1]), og = sigmoid_cell2(pre[2]);
+        const float2v ug = tanh_cell2(pre[3]);
+        const float2v cv = pp ? float2v{cold.z, cold.w} : float2v{cold.x, cold.y};
+        const float2v c2 = ig * ug + fg * cv;
+        const float2v h2 = og * tanh_cell2(c2);
+        gs = fma2(h2, fld(12), gs);
+        const _Float16 hi0 = (_Float16)h2.x, hi1 = (_Float16)h2.y;
+        const _Float16 lo0 = (_Float16)(h2.x - (float)hi0), lo1 = (_Float16)(h2.y - (float)hi1);
+        if (pp == 0) {
+          cnew.x = c2.x; cnew.y = c2.y; hnew.x = h2.x; hnew.y = h2.y;
+          hhi[0] = hi0; hhi[1] = hi1; hlo[0] = lo0; hlo[1] = lo1;
+        } else {
+          cnew.z = c2.x; cnew.w = c2.y; hnew.z = h2.x; hnew.w = h2.y;
+          hhi[2] = hi0; hhi[3] = hi1; hlo[2] = lo0; hlo[3] = lo1;
+        }
       }
       if (ok4) {
         *reinterpret_cast<float4*>(a.Cn + R * h + j0) = cnew;
@@ -234,6 +243,7 @@ __global__ __launch_bounds__(256, 2) void cell_f16x3_kernel(CellF16x3Args a) {
         *reinterpret_cast<half4*>(a.Hn16 + MH + R * h + j0) = hlo;
       }
     }
+    float gsum = gs.x + gs.y;
     gsum += __shfl_xor(gsum, 32, 64);
     if (hf == 0 && rok) a.part[(int64_t)jt * M + R] = gsum;
   }

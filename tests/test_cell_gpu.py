@@ -64,3 +64,31 @@ def test_cell_matches_fp64(M, h):
     # deterministic: a second launch is bitwise identical
     Hn2, Cn2, part2 = ops.lstm_cell(H.cuda(), C.cuda(), xv.cuda(), g.cuda(), Upk, Wx)
     assert torch.equal(Hn, Hn2) and torch.equal(Cn, Cn2) and torch.equal(part, part2)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mag", [1e2, 1e6, 1e30, float("inf")])
+def test_cell_saturated_gates(mag):
+    """Divergent solves drive xv and g (and so the gate pre-activations) to huge values: the gates
+    must saturate to 0 / 1 / -1 like torch.sigmoid / torch.tanh, never produce NaN (the fast exp's
+    fma correction once met inf * negative + inf here)."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from iadmm import ops
+    M, h = 300, 40
+    gen = torch.Generator().manual_seed(5)
+    p = _params(h, 0.3, gen)
+    H = torch.tanh(torch.randn(M, h, generator=gen))
+    C = torch.randn(M, h, generator=gen)
+    sign = torch.where(torch.rand(M, generator=gen) < 0.5, -1.0, 1.0)
+    xv, g = sign * mag, -sign * mag * torch.rand(M, generator=gen)
+    dev = {k: v.cuda() for k, v in p.items()}
+    Upk, Wx = ops.lstm_pack(dev, h)
+    Hn, Cn, part = ops.lstm_cell(H.cuda(), C.cuda(), xv.cuda(), g.cuda(), Upk, Wx)
+    torch.cuda.synchronize()
+    Href, Cref, _ = _cell_fp64(p, H, C, xv, g)
+    ok = torch.isfinite(Cref)            # inf - inf in the fp64 reference's C is not a kernel error
+    assert not torch.isnan(Hn.cpu()[ok]).any() and not torch.isnan(Cn.cpu()[ok]).any()
+    assert float((Hn.double().cpu() - Href).abs()[ok].max()) < 1e-5
+    fin = ok & (Cref.abs() < 1e30)
+    assert rel(Cn.cpu()[fin], Cref[fin]) < 1e-5
