@@ -5,7 +5,7 @@ shape (n = 1000, 500 + 500 rows, N = 2000, B = 1024 per GPU), inputs resident in
 
 Prints one JSON line: instances/s of the whole Stage II, the factor and per-iteration times,
 the LU trailing-update and solve kernels against the HBM roofline (algorithmic bytes: the
-right-looking update reads and writes the trailing matrix once per panel; a solve reads L and U
+rank-64 trailing update reads and writes the trailing matrix once per 64-column block; a solve reads L and U
 once), and the CPU reference path (torch.linalg.lu_factor / lu_solve, the oracle) timed on a
 bounded sample on the host.
 
@@ -24,12 +24,12 @@ sys.path.insert(0, ROOT)
 import torch  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0
-LU_PANEL = 16  # csrc/lu.hip kNB
+LU_BLOCK = 64  # csrc/lu.hip kBlk: rank of the MFMA trailing update
 
 
-def update_bytes(N, nb=LU_PANEL):
-    """Algorithmic HBM bytes of the right-looking trailing updates of one N x N factorization:
-    A22 read + written, L21 and U12 read, once per panel."""
+def update_bytes(N, nb=LU_BLOCK):
+    """Algorithmic HBM bytes of the rank-64 trailing updates of one N x N factorization:
+    A22 read + written, L21 and U12 read, once per 64-column block."""
     tot = 0.0
     for k0 in range(0, N, nb):
         rest = N - k0 - nb

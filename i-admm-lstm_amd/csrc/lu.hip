@@ -1,35 +1,89 @@
 // Stage II: batched dense LU with partial pivoting and the two triangular solves
 // (reference: models/lu.py:26-35, torch.lu / torch.lu_solve on K[B,N,N]).
 //
-// Right-looking blocked LU, panel width kNB = 16, one panel step = two launches:
-//   lu_panel_kernel   one workgroup per instance: the (N-k) x 16 panel is factored in LDS
-//                     (pivot = first max |a| like LAPACK i?amax; the multipliers use a
-//                     reciprocal like ?getf2), the row interchanges are applied to the columns
-//                     left and right of the panel (?laswp), and U12 = L11^-1 A12 is solved.
-//   lu_update_kernel  B x ceil(rows/64) workgroups: A22 -= L21 U12, each thread owning a 4-column
-//                     group with its 16x4 slice of U12 in registers, rows streamed with 16-B
-//                     loads (HBM-bound: A22 read and written once per panel).
+// Right-looking blocked LU in 64-column blocks (the ?getrf structure), each block factored as
+// four 16-column panels:
+//   lu_panel_kernel        one workgroup per instance: the (N-k) x 16 panel is factored in LDS
+//                          (pivot = first max |a| like LAPACK i?amax; the multipliers use a
+//                          reciprocal like ?getf2), the row interchanges are applied to the
+//                          block's other columns (?laswp), and U = L11^-1 A is solved for the
+//                          panel rows inside the current 64-column block.
+//   lu_update_block_kernel A -= L21 U12 on the columns of the current block right of the panel
+//                          (<= 48 columns, rows below the panel).
+// and, once per block, on the columns right of it:
+//   lu_swap_trsm_block_kernel the block's row interchanges on the columns outside it, and
+//                          U12 = L11^-1 A12 for its 64 rows (L11 in LDS; one thread per column).
+//   lu_trail_kernel        A22 -= L21 U12, rank 64, on fp32 MFMA (v_mfma_f32_32x32x2f32): 128-column
+//                          strips streamed in 64-row steps, U12^T and -L21 staged in LDS, A22
+//                          loaded into the accumulators and stored back (A22 read + written once
+//                          per 64 columns instead of once per 16: a quarter of the HBM traffic of
+//                          a 16-wide right-looking update).
 // lu_solve_kernel: one workgroup per instance; P b, then blocked forward (unit L) and backward
 // (U) substitution: 64-row blocks, prefix dot products over coalesced row segments, the 64x64
 // diagonal block solved inside one wave.
 //
 // Pivots are stored 0-based (global row index swapped with row i).  info[b] = first i+1 with a
 // zero pivot (0 = non-singular), LAPACK convention.
+#include <algorithm>
+#include <type_traits>
+
 #include "common.h"
 
 namespace iadmm {
+
+typedef float floatx16 __attribute__((ext_vector_type(16)));
 
 constexpr int kNB = 16;
 constexpr int kPS = kNB + 1;       // LDS panel row stride (conflict-free column reads)
 constexpr int kLuThreads = 256;
 constexpr int kUpdRows = 64;
 constexpr int kSolveBlk = 64;
+constexpr int kBlk = 64;          // outer block width = rank of the trailing update
+constexpr int kTC = 128;          // trailing update: columns per workgroup strip
+constexpr int kTRS = 64;          //   rows per pipeline step
+constexpr int kTRW = 1024;        //   rows per workgroup
+constexpr int kTS = kBlk + 4;     //   LDS row stride of the staged U12^T / -L21 blocks
+constexpr int kCS = kTC + 8;      //   LDS row stride of the A22 staging tiles (conflict-free acc access)
+constexpr int kTrailThreads = 512;
+constexpr size_t kTrailLds = ((kTC + 2 * kTRS) * kTS + 2 * kTRS * kCS) * sizeof(float);
 
-__global__ __launch_bounds__(kLuThreads) void lu_panel_kernel(int N, int k0, float* A, int* piv, int* info) {
+// The net row permutation of n interchanges (row base + j <-> pv[j], in order, ?laswp):
+// afterwards row rowid[i] holds what row cur[i] held before, for i < *cnt (<= 2n; rowid[i] =
+// base + i for i < n).  Built by wave 0 in LDS (lane-parallel search with a ballot); the caller
+// moves each column with all loads before all stores, one memory latency instead of n.
+IADMM_DEV void build_row_perm(const int* pv, int base, int n, int* rowid, int* cur, int* cnt) {
+  const int lane = threadIdx.x & 63;
+  if ((threadIdx.x >> 6) == 0) {
+    for (int i = lane; i < n; i += 64) { rowid[i] = base + i; cur[i] = base + i; }
+    int c = n;
+    for (int j = 0; j < n; ++j) {
+      const int p = pv[j];
+      if (p == base + j) continue;
+      int found = -1;
+      for (int s0 = 0; s0 < c && found < 0; s0 += 64) {
+        const unsigned long long m = __ballot(s0 + lane < c && rowid[s0 + lane] == p);
+        if (m) found = s0 + __ffsll((long long)m) - 1;
+      }
+      if (found < 0) {
+        if (lane == 0) { rowid[c] = p; cur[c] = p; }
+        found = c++;
+      }
+      if (lane == 0) { const int t = cur[j]; cur[j] = cur[found]; cur[found] = t; }
+    }
+    if (lane == 0) *cnt = c;
+  }
+  __syncthreads();
+}
+
+__global__ __launch_bounds__(kLuThreads) void lu_panel_kernel(int N, int K0, int k0, int cend, float* A, int* piv, int* info) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   float* P = sm;                             // (N-k0) x kPS
   float* rv = P + (size_t)(N - k0) * kPS;    // reduction scratch: 4 waves x (val, idx)
   int* ri = reinterpret_cast<int*>(rv + 8);
+  int* pvs = ri + 8;                         // this panel's pivots, then its row permutation
+  int* prow = pvs + kNB;
+  int* pcur = prow + 2 * kNB;
+  int* pcnt = pcur + 2 * kNB;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const size_t b = blockIdx.x;
   float* Ab = A + b * (size_t)N * N;
@@ -77,6 +131,7 @@ __global__ __launch_bounds__(kLuThreads) void lu_panel_kernel(int N, int k0, flo
       if (bx >= R) bx = j;  // all entries NaN: keep the diagonal
       ri[4] = bx;
       piv[b * N + k0 + j] = k0 + bx;
+      pvs[j] = k0 + bx;
       if (P[bx * kPS + j] == 0.f && info[b] == 0) info[b] = k0 + j + 1;
     }
     __syncthreads();
@@ -113,43 +168,28 @@ __global__ __launch_bounds__(kLuThreads) void lu_panel_kernel(int N, int k0, flo
       Ab[(size_t)(k0 + r) * N + k0 + c] = P[r * kPS + c];
     }
   }
-  // Row interchanges on the columns outside the panel, in pivot order (?laswp), then
-  // U12 = L11^-1 A12 (unit lower forward substitution).  Thread t owns columns t + 256 u: it
-  // applies all interchanges to them in order (no barrier between interchanges) with the loads
-  // of kSwapCols columns in flight together; the TRSM then solves two columns at a time with
-  // their 16 loads issued before the substitution (one memory latency per step instead of one
-  // per element: this phase was latency-bound).
-  constexpr int kSwapCols = 8;
-  int pv[kNB];
+  // Row interchanges (?laswp) on the columns of the current 64-column block outside the panel
+  // (the columns left and right of the block get the whole block's interchanges at once in
+  // lu_swap_trsm_block_kernel), then U = L11^-1 A on the panel rows for the columns
+  // [k0 + nb, cend) of the block (unit lower forward substitution; two columns per thread with
+  // their 16 loads issued before the substitution).
+  build_row_perm(pvs, k0, nb, prow, pcur, pcnt);
+  {
+    const int cnt = *pcnt;
+    const int col = K0 + tid;
+    if (col < cend && (col < k0 || col >= k0 + nb)) {
+      float v[2 * kNB];
 #pragma unroll
-  for (int j = 0; j < kNB; ++j) pv[j] = j < nb ? piv[b * N + k0 + j] : k0 + j;
-  for (int cb = 0; cb < N; cb += kSwapCols * kLuThreads) {
+      for (int i = 0; i < 2 * kNB; ++i) v[i] = i < cnt ? Ab[(size_t)pcur[i] * N + col] : 0.f;
 #pragma unroll
-    for (int j = 0; j < kNB; ++j) {
-      const int rj = k0 + j, p = pv[j];
-      if (j >= nb || p == rj) continue;
-      float t0[kSwapCols], t1[kSwapCols];
-#pragma unroll
-      for (int u = 0; u < kSwapCols; ++u) {
-        const int c = cb + tid + kLuThreads * u;
-        const bool ok = c < N && (c < k0 || c >= k0 + nb);
-        t0[u] = ok ? Ab[(size_t)rj * N + c] : 0.f;
-        t1[u] = ok ? Ab[(size_t)p * N + c] : 0.f;
-      }
-#pragma unroll
-      for (int u = 0; u < kSwapCols; ++u) {
-        const int c = cb + tid + kLuThreads * u;
-        if (c < N && (c < k0 || c >= k0 + nb)) {
-          Ab[(size_t)rj * N + c] = t1[u];
-          Ab[(size_t)p * N + c] = t0[u];
-        }
-      }
+      for (int i = 0; i < 2 * kNB; ++i)
+        if (i < cnt) Ab[(size_t)prow[i] * N + col] = v[i];
     }
   }
   __syncthreads();  // the TRSM's column owners differ from the interchanges' (c - k0 - nb vs c)
-  for (int c = k0 + nb + tid; c < N; c += 2 * kLuThreads) {
+  for (int c = k0 + nb + tid; c < cend; c += 2 * kLuThreads) {
     const int c2 = c + kLuThreads;
-    const bool ok2 = c2 < N;
+    const bool ok2 = c2 < cend;
     float x[kNB], x2[kNB];
 #pragma unroll
     for (int i = 0; i < kNB; ++i) {
@@ -177,55 +217,253 @@ __global__ __launch_bounds__(kLuThreads) void lu_panel_kernel(int N, int k0, flo
   }
 }
 
-// A22 -= L21 U12 for rows [k0+16 + blockIdx.y*64, +64) of instance blockIdx.x.
-template <bool VEC>
-__global__ __launch_bounds__(256) void lu_update_kernel(int N, int k0, float* A) {
-  __shared__ float Ls[kUpdRows][kNB];
-  const int nb = kNB;
+// A[c0.., c0..cend) -= L21 U12 inside the current 64-column block, c0 = k0 + 16: rows
+// [c0 + blockIdx.y*64, +64) of instance blockIdx.x, w = cend - c0 <= 48 columns.
+__global__ __launch_bounds__(256) void lu_update_block_kernel(int N, int k0, int cend, float* A) {
+  __shared__ float Us[kNB][kBlk - kNB];
+  __shared__ float Ls[kUpdRows][kNB + 1];
+  const int tid = threadIdx.x;
   const size_t b = blockIdx.x;
   float* Ab = A + b * (size_t)N * N;
-  const int c0 = k0 + nb;
+  const int c0 = k0 + kNB, w = cend - c0;
   const int r0 = c0 + blockIdx.y * kUpdRows;
   const int rows = min(kUpdRows, N - r0);
-  if (rows <= 0) return;
-  for (int idx = threadIdx.x; idx < rows * nb; idx += blockDim.x) {
-    const int r = idx / nb, l = idx % nb;
+  if (rows <= 0 || w <= 0) return;
+  for (int idx = tid; idx < kNB * w; idx += blockDim.x) {
+    const int l = idx / w, c = idx % w;
+    Us[l][c] = Ab[(size_t)(k0 + l) * N + c0 + c];
+  }
+  for (int idx = tid; idx < rows * kNB; idx += blockDim.x) {
+    const int r = idx / kNB, l = idx % kNB;
     Ls[r][l] = Ab[(size_t)(r0 + r) * N + k0 + l];
   }
   __syncthreads();
-  if constexpr (VEC) {
-    const int ncg = (N - c0) / 4;  // c0 and N are multiples of 4
-    for (int cg = threadIdx.x; cg < ncg; cg += blockDim.x) {
-      const int c = c0 + 4 * cg;
-      float4 u[kNB];
+  const int tot = rows * w;
+#pragma unroll 4
+  for (int idx = tid; idx < tot; idx += blockDim.x) {
+    const int r = idx / w, c = idx % w;
+    float* ap = Ab + (size_t)(r0 + r) * N + c0 + c;
+    float a = *ap;
 #pragma unroll
-      for (int l = 0; l < kNB; ++l) u[l] = *reinterpret_cast<const float4*>(Ab + (size_t)(k0 + l) * N + c);
-      // (HBM-bound on the read + write of A22: software-pipelining the rows or batching four
-      // measured no gain, bench_stage2.py; a wider panel is what would halve the traffic)
-      for (int r = 0; r < rows; ++r) {
-        float4* ap = reinterpret_cast<float4*>(Ab + (size_t)(r0 + r) * N + c);
-        float4 a = *ap;
+    for (int l = 0; l < kNB; ++l) a = a - Ls[r][l] * Us[l][c];
+    *ap = a;
+  }
+}
+
+// Once per 64-column block [K0, cend): the net row permutation of its interchanges, one wave per
+// instance, into perm[b] = {rowid[128], cur[128], cnt} (kPermInts ints).
+constexpr int kPermInts = 4 * kBlk + 1;
+__global__ __launch_bounds__(64) void lu_block_perm_kernel(int N, int K0, int cend, const int* piv, int* perm) {
+  __shared__ int pvs[kBlk], prow[2 * kBlk], pcur[2 * kBlk], pcnt[1];
+  const int tid = threadIdx.x, nbk = cend - K0;
+  const size_t b = blockIdx.x;
+  if (tid < nbk) pvs[tid] = piv[b * N + K0 + tid];
+  __syncthreads();
+  build_row_perm(pvs, K0, nbk, prow, pcur, pcnt);
+  int* out = perm + b * kPermInts;
+  for (int i = tid; i < 2 * kBlk; i += 64) { out[i] = prow[i]; out[2 * kBlk + i] = pcur[i]; }
+  if (tid == 0) out[4 * kBlk] = *pcnt;
+}
+
+// Once per block: its row interchanges on the columns outside it (the final L left of it, A12 /
+// A22 right of it), and for the right columns U12 = L11^-1 A12 on the block rows (L11 = the
+// block's unit-lower multipliers, in LDS, broadcast reads).  One thread per column.  Every row
+// outside the block that the interchanges touch ends up holding an original block row, so: the
+// new block rows are loaded first (x, registers), then the outside rows are moved 16 at a time
+// (their sources are block rows, which are only stored to afterwards), then the substitution and
+// the block-row stores.  Column index space: [0, K0) then [cend, N).
+__global__ __launch_bounds__(256) void lu_swap_trsm_block_kernel(int N, int K0, int cend, float* A, const int* perm) {
+  __shared__ float Ld[kBlk][kBlk + 1];
+  __shared__ int prow[2 * kBlk], pcur[2 * kBlk], pcnt[1];
+  const int tid = threadIdx.x;
+  const size_t b = blockIdx.x;
+  float* Ab = A + b * (size_t)N * N;
+  const int nbk = cend - K0;
+  if (cend < N)
+    for (int idx = tid; idx < kBlk * kBlk; idx += blockDim.x) {
+      const int r = idx / kBlk, c = idx % kBlk;
+      Ld[r][c] = Ab[(size_t)(K0 + r) * N + K0 + c];
+    }
+  const int* pb = perm + b * kPermInts;
+  if (tid < 2 * kBlk) { prow[tid] = pb[tid]; pcur[tid] = pb[2 * kBlk + tid]; }
+  if (tid == 0) *pcnt = pb[4 * kBlk];
+  __syncthreads();
+  const int cnt = *pcnt;
+  const int q = blockIdx.y * blockDim.x + tid;
+  const int c = q < K0 ? q : cend + (q - K0);
+  if (c >= N) return;
+  float x[kBlk];
 #pragma unroll
-        for (int l = 0; l < kNB; ++l) {
-          const float lv = Ls[r][l];
-          a.x = a.x - lv * u[l].x; a.y = a.y - lv * u[l].y;
-          a.z = a.z - lv * u[l].z; a.w = a.w - lv * u[l].w;
-        }
-        *ap = a;
+  for (int i = 0; i < kBlk; ++i) x[i] = i < nbk ? Ab[(size_t)pcur[i] * N + c] : 0.f;
+  for (int i0 = nbk; i0 < cnt; i0 += 16) {
+    float y[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) y[i] = i0 + i < cnt ? Ab[(size_t)pcur[i0 + i] * N + c] : 0.f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i)
+      if (i0 + i < cnt) Ab[(size_t)prow[i0 + i] * N + c] = y[i];
+  }
+  if (c >= cend) {  // right of the block: nbk == kBlk
+#pragma unroll
+    for (int i = 1; i < kBlk; ++i) {
+      float s = x[i];
+#pragma unroll
+      for (int l = 0; l < i; ++l) s = s - Ld[i][l] * x[l];
+      x[i] = s;
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < kBlk; ++i)
+    if (i < nbk) Ab[(size_t)(K0 + i) * N + c] = x[i];
+}
+
+// A22 -= L21 U12 (rank 64) on the trailing matrix [c0, N)^2, c0 = K0 + 64.  A workgroup (8 waves,
+// one per CU) owns a 128-column strip [cb, cb + 128) over kTRW rows [rs, re): U12's 64 x 128
+// block is staged once, transposed, in LDS (Ut); the rows are streamed in steps of 64 with a
+// one-step software pipeline.  A22 moves between HBM and the accumulators through LDS (Cin /
+// Cout) so that the global accesses are row-contiguous 16-B lanes (512 B per row per half-wave:
+// the MFMA layout's own 2-rows-x-128-B dword pattern ran at a third of that rate); -L21 is
+// double-buffered in LDS (Ls).  Wave (wr, wc) owns 32 x 32 of a step = one
+// v_mfma_f32_32x32x2f32 accumulator; both operands are 16-B LDS reads along k: lane half h covers
+// k in [32h, 32h + 32) and MFMA step s uses k = 32h + s (any k order gives the same sum set).  The
+// strips of one instance are consecutive logical ids on one XCD (its L2 serves the -L21 re-reads
+// of the 16 strips).  VEC: N % 4 == 0 and 16-B aligned rows (16-B global accesses).
+// DIAG (tools/lubench.hip only): 1 = no MFMAs (the memory pipeline alone).
+template <bool VEC, int DIAG = 0>
+__global__ __launch_bounds__(kTrailThreads, 1) void lu_trail_kernel(int N, int K0, int ntc, int nrc, float* A) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  float* Ut = sm;                       // [kTC cols][kTS]: U12^T
+  float* Lsb = Ut + kTC * kTS;          // 2 x [kTRS rows][kTS]: -L21
+  float* Cin = Lsb + 2 * kTRS * kTS;    // [kTRS rows][kCS]: next step's A22 rows
+  float* Cout = Cin + kTRS * kCS;       // [kTRS rows][kCS]: this step's result rows
+  const int nwg = gridDim.x, bid = blockIdx.x;
+  const int xcd = bid & 7, local = bid >> 3, q8 = nwg >> 3, r8 = nwg & 7;
+  const int logical = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + local;
+  const int per = ntc * nrc;
+  const size_t b = (size_t)(logical / per);
+  const int t = logical % per, rc = t / ntc, tc = t % ntc;
+  float* Ab = A + b * (size_t)N * N;
+  const int c0 = K0 + kBlk;
+  const int cb = c0 + tc * kTC, rs = c0 + rc * kTRW, re = min(N, rs + kTRW);
+  const int nsteps = (re - rs + kTRS - 1) / kTRS;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, il = lane & 31, h = lane >> 5;
+  const int wr = (wave >> 2) * 32, wc = (wave & 3) * 32;
+  constexpr int NT = kTrailThreads;
+
+  typedef typename std::conditional<VEC, float4, float>::type VT;
+  constexpr int W = VEC ? 4 : 1;                    // floats per global access
+  constexpr int kCQ = kTRS * kTC / W / NT;          // A22 accesses per thread per step
+  constexpr int kLQ = kTRS * kBlk / W / NT;         // -L21 accesses per thread per step
+  constexpr int kUQ = kBlk * kTC / W / NT;          // U12 accesses per thread
+  constexpr int CPR = kTC / W, LPR = kBlk / W;      // accesses per row
+  auto ld = [&](int row, int col, bool ok) -> VT {  // clamped address, masked value
+    const float* p = Ab + (size_t)row * N + col;
+    if constexpr (VEC) {
+      const float4 x = *reinterpret_cast<const float4*>(p);
+      return ok ? x : make_float4(0.f, 0.f, 0.f, 0.f);
+    } else {
+      const float x = *p;
+      return ok ? x : 0.f;
+    }
+  };
+  auto st_lds = [&](float* d, const VT& v, float sgn) {
+    if constexpr (VEC) *reinterpret_cast<float4*>(d) = make_float4(sgn * v.x, sgn * v.y, sgn * v.z, sgn * v.w);
+    else *d = sgn * v;
+  };
+  auto loadC = [&](int step, VT (&c)[kCQ]) {
+#pragma unroll
+    for (int q = 0; q < kCQ; ++q) {
+      const int e = tid + NT * q, row = rs + step * kTRS + e / CPR, col = cb + (e % CPR) * W;
+      c[q] = ld(min(row, re - 1), min(col, N - W), row < re && col < N);
+    }
+  };
+  auto loadL = [&](int step, VT (&l)[kLQ]) {
+#pragma unroll
+    for (int q = 0; q < kLQ; ++q) {
+      const int e = tid + NT * q, row = rs + step * kTRS + e / LPR;
+      l[q] = ld(min(row, re - 1), K0 + (e % LPR) * W, row < re);
+    }
+  };
+  auto writeC = [&](const VT (&c)[kCQ]) {
+#pragma unroll
+    for (int q = 0; q < kCQ; ++q) {
+      const int e = tid + NT * q;
+      st_lds(Cin + (e / CPR) * kCS + (e % CPR) * W, c[q], 1.f);
+    }
+  };
+  auto writeL = [&](int buf, const VT (&l)[kLQ]) {
+#pragma unroll
+    for (int q = 0; q < kLQ; ++q) {
+      const int e = tid + NT * q;
+      st_lds(Lsb + buf * kTRS * kTS + (e / LPR) * kTS + (e % LPR) * W, l[q], -1.f);
+    }
+  };
+  auto storeOut = [&](int step) {
+#pragma unroll
+    for (int q = 0; q < kCQ; ++q) {
+      const int e = tid + NT * q, row = rs + step * kTRS + e / CPR, col = cb + (e % CPR) * W;
+      if (row < re && col < N) {
+        const float* s = Cout + (e / CPR) * kCS + (e % CPR) * W;
+        if constexpr (VEC) *reinterpret_cast<float4*>(Ab + (size_t)row * N + col) = *reinterpret_cast<const float4*>(s);
+        else Ab[(size_t)row * N + col] = *s;
       }
     }
-  } else {
-    for (int c = c0 + threadIdx.x; c < N; c += blockDim.x) {
-      float u[kNB];
+  };
+  // accumulator register v <-> tile row wr + 8(v/4) + 4h + v%4, column wc + il
+  auto accFromCin = [&](floatx16& acc) {
 #pragma unroll
-      for (int l = 0; l < kNB; ++l) u[l] = Ab[(size_t)(k0 + l) * N + c];
-      for (int r = 0; r < rows; ++r) {
-        float a = Ab[(size_t)(r0 + r) * N + c];
+    for (int v = 0; v < 16; ++v) acc[v] = Cin[(wr + 8 * (v >> 2) + 4 * h + (v & 3)) * kCS + wc + il];
+  };
+  auto accToCout = [&](const floatx16& acc) {
 #pragma unroll
-        for (int l = 0; l < kNB; ++l) a = a - Ls[r][l] * u[l];
-        Ab[(size_t)(r0 + r) * N + c] = a;
+    for (int v = 0; v < 16; ++v) Cout[(wr + 8 * (v >> 2) + 4 * h + (v & 3)) * kCS + wc + il] = acc[v];
+  };
+
+  VT cr[kCQ], lr[kLQ];
+  loadC(0, cr);
+  loadL(0, lr);
+#pragma unroll
+  for (int q = 0; q < kUQ; ++q) {  // U12 block -> Ut (transposed)
+    const int e = tid + NT * q, k = e / CPR, cl = (e % CPR) * W, col = cb + cl;
+    const VT u = ld(K0 + k, min(col, N - W), col < N);
+    if constexpr (VEC) {
+      Ut[(cl + 0) * kTS + k] = u.x; Ut[(cl + 1) * kTS + k] = u.y;
+      Ut[(cl + 2) * kTS + k] = u.z; Ut[(cl + 3) * kTS + k] = u.w;
+    } else {
+      Ut[cl * kTS + k] = u;
+    }
+  }
+  writeC(cr);
+  writeL(0, lr);
+  __syncthreads();
+  floatx16 acc;
+  accFromCin(acc);
+
+  for (int step = 0; step < nsteps; ++step) {
+    const bool more = step + 1 < nsteps;
+    if (more) {
+      loadC(step + 1, cr);
+      loadL(step + 1, lr);
+    }
+    if constexpr (DIAG != 1) {
+      const float* Ls = Lsb + (step & 1) * kTRS * kTS;
+#pragma unroll
+      for (int sg = 0; sg < 8; ++sg) {
+        const float4 fa = *reinterpret_cast<const float4*>(Ls + (wr + il) * kTS + 32 * h + 4 * sg);
+        const float4 fb = *reinterpret_cast<const float4*>(Ut + (wc + il) * kTS + 32 * h + 4 * sg);
+#pragma unroll
+        for (int s4 = 0; s4 < 4; ++s4) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(get4(fa, s4), get4(fb, s4), acc, 0, 0, 0);
       }
     }
+    accToCout(acc);
+    __syncthreads();  // Cin (this step's rows) and Ls[step & 1] fully consumed, Cout complete
+    if (more) {
+      writeC(cr);
+      writeL((step + 1) & 1, lr);
+    }
+    storeOut(step);
+    __syncthreads();  // Cout drained, Cin / Ls hold the next step
+    if (more) accFromCin(acc);
   }
 }
 
@@ -336,27 +574,59 @@ __global__ void kkt_rhs_kernel(int64_t B, int n, int m, int num_ineq, const floa
 
 using namespace iadmm;
 
+static int lu_factor_blocks(int64_t B, int64_t N, float* A, int* piv, int* info, int* perm, size_t lds,
+                            hipStream_t s) {
+  const bool vec = (N % 4 == 0) && aligned16(A);
+  IADMM_ALLOW_LDS(lu_trail_kernel<true>, kTrailLds);
+  IADMM_ALLOW_LDS(lu_trail_kernel<false>, kTrailLds);
+  for (int K0 = 0; K0 < N; K0 += kBlk) {
+    const int cend = (int)std::min<int64_t>(N, K0 + kBlk);
+    for (int k0 = K0; k0 < cend; k0 += kNB) {
+      hipLaunchKernelGGL(lu_panel_kernel, dim3((unsigned)B), dim3(kLuThreads), lds, s, (int)N, K0, k0, cend, A, piv, info);
+      IADMM_CHECK_LAUNCH();
+      const int c0 = k0 + kNB;
+      if (c0 < cend) {
+        const dim3 grid((unsigned)B, (unsigned)((N - c0 + kUpdRows - 1) / kUpdRows));
+        hipLaunchKernelGGL(lu_update_block_kernel, grid, dim3(256), 0, s, (int)N, k0, cend, A);
+        IADMM_CHECK_LAUNCH();
+      }
+    }
+    const int outside = K0 + ((int)N - cend);
+    if (outside > 0) {
+      hipLaunchKernelGGL(lu_block_perm_kernel, dim3((unsigned)B), dim3(64), 0, s, (int)N, K0, cend, piv, perm);
+      IADMM_CHECK_LAUNCH();
+      hipLaunchKernelGGL(lu_swap_trsm_block_kernel, dim3((unsigned)B, (unsigned)((outside + 255) / 256)), dim3(256), 0,
+                         s, (int)N, K0, cend, A, perm);
+      IADMM_CHECK_LAUNCH();
+    }
+    if (cend < N) {
+      const int rest = (int)N - cend;
+      const int ntc = (rest + kTC - 1) / kTC, nrc = (rest + kTRW - 1) / kTRW;
+      const dim3 grid((unsigned)(B * ntc * nrc));
+      if (vec) hipLaunchKernelGGL(lu_trail_kernel<true>, grid, dim3(kTrailThreads), kTrailLds, s, (int)N, K0, ntc, nrc, A);
+      else hipLaunchKernelGGL(lu_trail_kernel<false>, grid, dim3(kTrailThreads), kTrailLds, s, (int)N, K0, ntc, nrc, A);
+      IADMM_CHECK_LAUNCH();
+    }
+  }
+  return 0;
+}
+
 extern "C" int iadmm_lu_factor(int64_t B, int64_t N, float* A, int* piv, int* info, void* stream) {
   if (B <= 0 || N <= 0 || !A || !piv || !info) return IADMM_E_ARG;
-  const size_t lds = ((size_t)N * kPS + 16) * sizeof(float);
+  const size_t lds = ((size_t)N * kPS + 16 + 7 * kNB) * sizeof(float);
   if (lds > 160 * 1024 || B > 0x7fffffff) return IADMM_E_SIZE;
   hipStream_t s = (hipStream_t)stream;
   IADMM_ALLOW_LDS(lu_panel_kernel, lds);
   hipError_t e = hipMemsetAsync(info, 0, B * sizeof(int), s);
   if (e != hipSuccess) return (int)e;
-  const bool vec = (N % 4 == 0) && aligned16(A);
-  for (int k0 = 0; k0 < N; k0 += kNB) {
-    hipLaunchKernelGGL(lu_panel_kernel, dim3((unsigned)B), dim3(kLuThreads), lds, s, (int)N, k0, A, piv, info);
-    IADMM_CHECK_LAUNCH();
-    const int rest = (int)N - k0 - kNB;
-    if (rest > 0) {
-      const dim3 grid((unsigned)B, (unsigned)((rest + kUpdRows - 1) / kUpdRows));
-      if (vec) hipLaunchKernelGGL(lu_update_kernel<true>, grid, dim3(256), 0, s, (int)N, k0, A);
-      else hipLaunchKernelGGL(lu_update_kernel<false>, grid, dim3(256), 0, s, (int)N, k0, A);
-      IADMM_CHECK_LAUNCH();
-    }
-  }
-  return 0;
+  const int64_t ntc_max = (N + kTC - 1) / kTC, nrc_max = (N + kTRW - 1) / kTRW;
+  if (B * ntc_max * nrc_max > 0x7fffffff) return IADMM_E_SIZE;
+  int* perm = nullptr;  // per-instance block permutations (stream-ordered scratch)
+  e = hipMallocAsync((void**)&perm, (size_t)B * kPermInts * sizeof(int), s);
+  if (e != hipSuccess) return (int)e;
+  const int rc = lu_factor_blocks(B, N, A, piv, info, perm, lds, s);
+  e = hipFreeAsync(perm, s);
+  return rc != 0 ? rc : (int)e;
 }
 
 extern "C" int iadmm_lu_solve(int64_t B, int64_t N, const float* LU, const int* piv, float* x,

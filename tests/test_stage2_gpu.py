@@ -26,7 +26,9 @@ def _gpu():
         pytest.skip("no GPU")
 
 
-@pytest.mark.parametrize("N,B", [(16, 2), (37, 3), (64, 2), (100, 2), (400, 2), (2000, 1)])
+# 16 / 37 / 64: one 64-column block; 100, 130, 257 (N % 4 != 0: scalar trailing-update loads),
+# 400, 2000: several blocks with partial 128 x 128 trailing tiles
+@pytest.mark.parametrize("N,B", [(16, 2), (37, 3), (64, 2), (100, 2), (130, 2), (257, 2), (400, 2), (2000, 1)])
 def test_lu_factor_solve_backward_error(N, B):
     from iadmm import ops
     g = torch.Generator().manual_seed(N)
