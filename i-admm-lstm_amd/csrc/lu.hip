@@ -3,7 +3,7 @@
 //
 // Right-looking blocked LU in 64-column blocks (the ?getrf structure), each block factored as
 // four 16-column panels:
-//   lu_panel_kernel        one workgroup per instance: the (N-k) x 16 panel is factored in LDS
+//   lu_panel_kernel        one workgroup per instance: the (N-k) x 16 panel is factored in registers
 //                          (pivot = first max |a| like LAPACK i?amax; the multipliers use a
 //                          reciprocal like ?getf2), the row interchanges are applied to the
 //                          block's other columns (?laswp), and U = L11^-1 A is solved for the
@@ -34,7 +34,7 @@ namespace iadmm {
 typedef float floatx16 __attribute__((ext_vector_type(16)));
 
 constexpr int kNB = 16;
-constexpr int kPS = kNB + 1;       // LDS panel row stride (conflict-free column reads)
+constexpr int kPanelMaxM = 12;     // panel rows per thread: N <= 12 * 256
 constexpr int kLuThreads = 256;
 constexpr int kUpdRows = 64;
 constexpr int kSolveBlk = 64;
@@ -75,45 +75,64 @@ IADMM_DEV void build_row_perm(const int* pv, int base, int n, int* rowid, int* c
   __syncthreads();
 }
 
-__global__ __launch_bounds__(kLuThreads) void lu_panel_kernel(int N, int K0, int k0, int cend, float* A, int* piv, int* info) {
-  extern __shared__ __attribute__((aligned(16))) float sm[];
-  float* P = sm;                             // (N-k0) x kPS
-  float* rv = P + (size_t)(N - k0) * kPS;    // reduction scratch: 4 waves x (val, idx)
-  int* ri = reinterpret_cast<int*>(rv + 8);
-  int* pvs = ri + 8;                         // this panel's pivots, then its row permutation
-  int* prow = pvs + kNB;
-  int* pcur = prow + 2 * kNB;
-  int* pcnt = pcur + 2 * kNB;
+// The (N-k0) x 16 panel lives in registers: thread t owns rows t + 256 m (m < M), 16 columns
+// each.  Per column j: argmax |a| (thread scan, wave shuffle tree, 4-wave combine in LDS; first
+// index on ties), the owners of rows j and p exchange them through LDS, every thread scales its
+// rows below j by the reciprocal and applies the rank-1 update in registers.  M = ceil((N-k0)/256)
+// rounded up to the next instantiated size.
+IADMM_DEV float col_of(const float (&row)[kNB], int j) {  // row[j] for a run-time j, registers only
+  float v = row[0];
+#pragma unroll
+  for (int c = 1; c < kNB; ++c) v = c == j ? row[c] : v;
+  return v;
+}
+
+template <int M>
+__global__ __launch_bounds__(kLuThreads, 2) void lu_panel_kernel(int N, int K0, int k0, int cend, float* A, int* piv,
+                                                                  int* info) {
+  __shared__ float xrow[2][kNB];            // [0] = row j, [1] = pivot row (after the exchange: row j)
+  __shared__ float L11[kNB][kNB + 1];
+  __shared__ float rv[4];
+  __shared__ int ri[5];
+  __shared__ int pvs[kNB], prow[2 * kNB], pcur[2 * kNB], pcnt[1];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const size_t b = blockIdx.x;
   float* Ab = A + b * (size_t)N * N;
   const int R = N - k0;
   const int nb = min(kNB, R);
-
-  // 16-B loads when the panel is a whole 16-column block of 16-B-aligned rows
   const bool vec = nb == kNB && (N % 4) == 0 && aligned16(Ab);
-  if (vec) {
-#pragma unroll 4
-    for (int q = tid; q < R * 4; q += blockDim.x) {
-      const int r = q >> 2, c4 = (q & 3) * 4;
-      const float4 v = *reinterpret_cast<const float4*>(Ab + (size_t)(k0 + r) * N + k0 + c4);
-      P[r * kPS + c4] = v.x; P[r * kPS + c4 + 1] = v.y; P[r * kPS + c4 + 2] = v.z; P[r * kPS + c4 + 3] = v.w;
+
+  float a[M][kNB];
+#pragma unroll
+  for (int m = 0; m < M; ++m) {
+    const int r = tid + kLuThreads * m;
+    const float* src = Ab + (size_t)(k0 + min(r, R - 1)) * N + k0;
+    if (vec) {
+#pragma unroll
+      for (int c4 = 0; c4 < kNB; c4 += 4) {
+        const float4 v = *reinterpret_cast<const float4*>(src + c4);
+        a[m][c4] = v.x; a[m][c4 + 1] = v.y; a[m][c4 + 2] = v.z; a[m][c4 + 3] = v.w;
+      }
+    } else {
+#pragma unroll
+      for (int c = 0; c < kNB; ++c) a[m][c] = c < nb ? src[c] : 0.f;
     }
-  } else {
-    for (int idx = tid; idx < R * nb; idx += blockDim.x) {
-      const int r = idx / nb, c = idx % nb;
-      P[r * kPS + c] = Ab[(size_t)(k0 + r) * N + k0 + c];
+    if (r >= R) {
+#pragma unroll
+      for (int c = 0; c < kNB; ++c) a[m][c] = 0.f;
     }
   }
-  __syncthreads();
 
-  for (int j = 0; j < nb; ++j) {
-    // pivot: first index of max |P[r][j]| over r in [j, R)
+#pragma unroll
+  for (int j = 0; j < kNB; ++j) {
+    if (j < nb) {
     float best = -1.f;
     int bi = R;
-    for (int r = j + tid; r < R; r += blockDim.x) {
-      const float v = fabsf(P[r * kPS + j]);
-      if (v > best) { best = v; bi = r; }
+#pragma unroll
+    for (int m = 0; m < M; ++m) {
+      const int r = tid + kLuThreads * m;
+      const float v = fabsf(col_of(a[m], j));
+      if (r >= j && r < R && v > best) { best = v; bi = r; }
     }
 #pragma unroll
     for (int o = 32; o >= 1; o >>= 1) {
@@ -122,58 +141,89 @@ __global__ __launch_bounds__(kLuThreads) void lu_panel_kernel(int N, int K0, int
       if (ov > best || (ov == best && oi < bi)) { best = ov; bi = oi; }
     }
     if (lane == 0) { rv[wave] = best; ri[wave] = bi; }
+    if (tid == j) {
+#pragma unroll
+      for (int c = 0; c < kNB; ++c) xrow[0][c] = a[0][c];
+    }
     __syncthreads();
     if (tid == 0) {
       float bv = rv[0];
       int bx = ri[0];
-      for (int w = 1; w < (int)(blockDim.x >> 6); ++w)
+      for (int w = 1; w < kLuThreads / 64; ++w)
         if (rv[w] > bv || (rv[w] == bv && ri[w] < bx)) { bv = rv[w]; bx = ri[w]; }
       if (bx >= R) bx = j;  // all entries NaN: keep the diagonal
+      else if (bv == 0.f && info[b] == 0) info[b] = k0 + j + 1;
       ri[4] = bx;
       piv[b * N + k0 + j] = k0 + bx;
       pvs[j] = k0 + bx;
-      if (P[bx * kPS + j] == 0.f && info[b] == 0) info[b] = k0 + j + 1;
     }
     __syncthreads();
     const int p = ri[4];
-    if (p != j && tid < nb) {
-      const float t = P[j * kPS + tid];
-      P[j * kPS + tid] = P[p * kPS + tid];
-      P[p * kPS + tid] = t;
-    }
+    // the owner of row p publishes it and takes row j's values
+#pragma unroll
+    for (int m = 0; m < M; ++m)
+      if (tid + kLuThreads * m == p) {
+#pragma unroll
+        for (int c = 0; c < kNB; ++c) {
+          xrow[1][c] = a[m][c];
+          a[m][c] = xrow[0][c];
+        }
+      }
     __syncthreads();
-    const float pv = P[j * kPS + j];
+    if (tid == j) {
+#pragma unroll
+      for (int c = 0; c < kNB; ++c) a[0][c] = xrow[1][c];
+    }
+    const float pv = xrow[1][j];
     if (pv != 0.f) {
       const float rcp = 1.0f / pv;
-      for (int r = j + 1 + tid; r < R; r += blockDim.x) {
-        const float l = P[r * kPS + j] * rcp;
-        P[r * kPS + j] = l;
-        for (int c = j + 1; c < nb; ++c) P[r * kPS + c] = P[r * kPS + c] - l * P[j * kPS + c];
+      float pr[kNB];
+#pragma unroll
+      for (int c = 0; c < kNB; ++c) pr[c] = xrow[1][c];
+#pragma unroll
+      for (int m = 0; m < M; ++m) {
+        const int r = tid + kLuThreads * m;
+        if (r > j && r < R) {
+          const float l = col_of(a[m], j) * rcp;
+#pragma unroll
+          for (int c = 0; c < kNB; ++c) {  // static register indices: j is not a compile-time constant
+            if (c == j) a[m][c] = l;
+            else if (c > j) a[m][c] = a[m][c] - l * pr[c];
+          }
+        }
       }
     }
-    __syncthreads();
+    __syncthreads();  // xrow is rewritten by the next column
+    }
   }
 
-  // write the factored panel back
-  if (vec) {
-#pragma unroll 4
-    for (int q = tid; q < R * 4; q += blockDim.x) {
-      const int r = q >> 2, c4 = (q & 3) * 4;
-      *reinterpret_cast<float4*>(Ab + (size_t)(k0 + r) * N + k0 + c4) =
-          make_float4(P[r * kPS + c4], P[r * kPS + c4 + 1], P[r * kPS + c4 + 2], P[r * kPS + c4 + 3]);
+  // write the factored panel back; L11 for the in-block substitution
+#pragma unroll
+  for (int m = 0; m < M; ++m) {
+    const int r = tid + kLuThreads * m;
+    if (r < R) {
+      float* dst = Ab + (size_t)(k0 + r) * N + k0;
+      if (vec) {
+#pragma unroll
+        for (int c4 = 0; c4 < kNB; c4 += 4)
+          *reinterpret_cast<float4*>(dst + c4) = make_float4(a[m][c4], a[m][c4 + 1], a[m][c4 + 2], a[m][c4 + 3]);
+      } else {
+#pragma unroll
+        for (int c = 0; c < kNB; ++c)
+          if (c < nb) dst[c] = a[m][c];
+      }
     }
-  } else {
-    for (int idx = tid; idx < R * nb; idx += blockDim.x) {
-      const int r = idx / nb, c = idx % nb;
-      Ab[(size_t)(k0 + r) * N + k0 + c] = P[r * kPS + c];
-    }
+  }
+  if (tid < nb) {
+#pragma unroll
+    for (int c = 0; c < kNB; ++c) L11[tid][c] = a[0][c];
   }
   // Row interchanges (?laswp) on the columns of the current 64-column block outside the panel
   // (the columns left and right of the block get the whole block's interchanges at once in
   // lu_swap_trsm_block_kernel), then U = L11^-1 A on the panel rows for the columns
-  // [k0 + nb, cend) of the block (unit lower forward substitution; two columns per thread with
-  // their 16 loads issued before the substitution).
-  build_row_perm(pvs, k0, nb, prow, pcur, pcnt);
+  // [k0 + nb, cend) of the block (unit lower forward substitution, one column per thread with
+  // its 16 loads issued before the substitution).
+  build_row_perm(pvs, k0, nb, prow, pcur, pcnt);  // (its barrier also publishes L11)
   {
     const int cnt = *pcnt;
     const int col = K0 + tid;
@@ -186,34 +236,22 @@ __global__ __launch_bounds__(kLuThreads) void lu_panel_kernel(int N, int K0, int
         if (i < cnt) Ab[(size_t)prow[i] * N + col] = v[i];
     }
   }
-  __syncthreads();  // the TRSM's column owners differ from the interchanges' (c - k0 - nb vs c)
-  for (int c = k0 + nb + tid; c < cend; c += 2 * kLuThreads) {
-    const int c2 = c + kLuThreads;
-    const bool ok2 = c2 < cend;
-    float x[kNB], x2[kNB];
+  __syncthreads();  // the substitution's column owners differ from the interchanges'
+  const int c = k0 + nb + tid;
+  if (c < cend) {
+    float x[kNB];
 #pragma unroll
-    for (int i = 0; i < kNB; ++i) {
-      x[i] = i < nb ? Ab[(size_t)(k0 + i) * N + c] : 0.f;
-      x2[i] = (i < nb && ok2) ? Ab[(size_t)(k0 + i) * N + c2] : 0.f;
-    }
+    for (int i = 0; i < kNB; ++i) x[i] = i < nb ? Ab[(size_t)(k0 + i) * N + c] : 0.f;
 #pragma unroll
-    for (int i = 0; i < kNB; ++i) {
-      float s = x[i], s2 = x2[i];
-      for (int l = 0; l < i; ++l) {
-        const float lv = P[i * kPS + l];
-        s = s - lv * x[l];
-        s2 = s2 - lv * x2[l];
-      }
+    for (int i = 1; i < kNB; ++i) {
+      float s = x[i];
+#pragma unroll
+      for (int l = 0; l < i; ++l) s = s - L11[i][l] * x[l];
       x[i] = s;
-      x2[i] = s2;
     }
 #pragma unroll
-    for (int i = 0; i < kNB; ++i) {
-      if (i < nb) {
-        Ab[(size_t)(k0 + i) * N + c] = x[i];
-        if (ok2) Ab[(size_t)(k0 + i) * N + c2] = x2[i];
-      }
-    }
+    for (int i = 0; i < kNB; ++i)
+      if (i < nb) Ab[(size_t)(k0 + i) * N + c] = x[i];
   }
 }
 
@@ -574,15 +612,20 @@ __global__ void kkt_rhs_kernel(int64_t B, int n, int m, int num_ineq, const floa
 
 using namespace iadmm;
 
-static int lu_factor_blocks(int64_t B, int64_t N, float* A, int* piv, int* info, int* perm, size_t lds,
-                            hipStream_t s) {
+static int lu_factor_blocks(int64_t B, int64_t N, float* A, int* piv, int* info, int* perm, hipStream_t s) {
   const bool vec = (N % 4 == 0) && aligned16(A);
   IADMM_ALLOW_LDS(lu_trail_kernel<true>, kTrailLds);
   IADMM_ALLOW_LDS(lu_trail_kernel<false>, kTrailLds);
   for (int K0 = 0; K0 < N; K0 += kBlk) {
     const int cend = (int)std::min<int64_t>(N, K0 + kBlk);
     for (int k0 = K0; k0 < cend; k0 += kNB) {
-      hipLaunchKernelGGL(lu_panel_kernel, dim3((unsigned)B), dim3(kLuThreads), lds, s, (int)N, K0, k0, cend, A, piv, info);
+      const int R = (int)N - k0;
+      const dim3 g((unsigned)B), t(kLuThreads);
+      if (R <= kLuThreads) hipLaunchKernelGGL(lu_panel_kernel<1>, g, t, 0, s, (int)N, K0, k0, cend, A, piv, info);
+      else if (R <= 2 * kLuThreads) hipLaunchKernelGGL(lu_panel_kernel<2>, g, t, 0, s, (int)N, K0, k0, cend, A, piv, info);
+      else if (R <= 4 * kLuThreads) hipLaunchKernelGGL(lu_panel_kernel<4>, g, t, 0, s, (int)N, K0, k0, cend, A, piv, info);
+      else if (R <= 8 * kLuThreads) hipLaunchKernelGGL(lu_panel_kernel<8>, g, t, 0, s, (int)N, K0, k0, cend, A, piv, info);
+      else hipLaunchKernelGGL(lu_panel_kernel<kPanelMaxM>, g, t, 0, s, (int)N, K0, k0, cend, A, piv, info);
       IADMM_CHECK_LAUNCH();
       const int c0 = k0 + kNB;
       if (c0 < cend) {
@@ -613,10 +656,8 @@ static int lu_factor_blocks(int64_t B, int64_t N, float* A, int* piv, int* info,
 
 extern "C" int iadmm_lu_factor(int64_t B, int64_t N, float* A, int* piv, int* info, void* stream) {
   if (B <= 0 || N <= 0 || !A || !piv || !info) return IADMM_E_ARG;
-  const size_t lds = ((size_t)N * kPS + 16 + 7 * kNB) * sizeof(float);
-  if (lds > 160 * 1024 || B > 0x7fffffff) return IADMM_E_SIZE;
+  if (N > kPanelMaxM * kLuThreads || B > 0x7fffffff) return IADMM_E_SIZE;
   hipStream_t s = (hipStream_t)stream;
-  IADMM_ALLOW_LDS(lu_panel_kernel, lds);
   hipError_t e = hipMemsetAsync(info, 0, B * sizeof(int), s);
   if (e != hipSuccess) return (int)e;
   const int64_t ntc_max = (N + kTC - 1) / kTC, nrc_max = (N + kTRW - 1) / kTRW;
@@ -624,7 +665,7 @@ extern "C" int iadmm_lu_factor(int64_t B, int64_t N, float* A, int* piv, int* in
   int* perm = nullptr;  // per-instance block permutations (stream-ordered scratch)
   e = hipMallocAsync((void**)&perm, (size_t)B * kPermInts * sizeof(int), s);
   if (e != hipSuccess) return (int)e;
-  const int rc = lu_factor_blocks(B, N, A, piv, info, perm, lds, s);
+  const int rc = lu_factor_blocks(B, N, A, piv, info, perm, s);
   e = hipFreeAsync(perm, s);
   return rc != 0 ? rc : (int)e;
 }
