@@ -255,25 +255,40 @@ __global__ __launch_bounds__(kKktThreads) void kkt_matvec_kernel(KktArgs a, cons
 }
 
 // Dense K (models/lstm.py:67-68, models/lu.py:123-124) for Stage II and explicit inspection.
-__global__ void kkt_assemble_kernel(int64_t B, int n, int m, int num_ineq, const float* Q,
-                                    const float* A0, float sigma, const float* scal,
-                                    const float* rho_rows, float* K) {
+// One 64 x 64 tile of K per workgroup (blockIdx.x = instance, blockIdx.y = tile): rows of K are
+// written as coalesced 256-B segments; the A0^T block is staged through LDS so that A0 is also read
+// along its rows (a direct per-element formula read it with stride n and ran at 1.3 TB/s).
+constexpr int kAsmT = 64;
+__global__ __launch_bounds__(256) void kkt_assemble_kernel(int n, int m, int num_ineq, int ntile, const float* Q,
+                                                           const float* A0, float sigma, const float* scal,
+                                                           const float* rho_rows, float* K) {
+  __shared__ float T[kAsmT][kAsmT + 1];
   const int N = n + m;
-  const int64_t tot = B * (int64_t)N * N;
+  const size_t b = blockIdx.x;
+  const int i0 = (blockIdx.y / ntile) * kAsmT, j0 = (blockIdx.y % ntile) * kAsmT;
+  const int tid = threadIdx.x;
+  const float* Qb = Q + b * (size_t)n * n;
+  const float* Ab = A0 + b * (size_t)m * n;
+  float* Kb = K + b * (size_t)N * N;
   const float irho_in = scal ? scal[IADMM_S_IRHO_IN] : 0.f, irho_eq = scal ? scal[IADMM_S_IRHO_EQ] : 0.f;
-  for (int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; k < tot;
-       k += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t b = k / ((int64_t)N * N);
-    const int rem = (int)(k - b * (int64_t)N * N);
-    const int i = rem / N, j = rem % N;
+  if (i0 < n && j0 + kAsmT > n) {  // the tile meets the A0^T block: T[jj][ii] = A0[j - n][i]
+    for (int idx = tid; idx < kAsmT * kAsmT; idx += blockDim.x) {
+      const int jj = idx / kAsmT, ii = idx % kAsmT, i = i0 + ii, j = j0 + jj;
+      if (i < n && j >= n && j < N) T[jj][ii] = Ab[(size_t)(j - n) * n + i];
+    }
+    __syncthreads();
+  }
+  for (int idx = tid; idx < kAsmT * kAsmT; idx += blockDim.x) {
+    const int ii = idx / kAsmT, jj = idx % kAsmT, i = i0 + ii, j = j0 + jj;
+    if (i >= N || j >= N) continue;
     float v;
-    if (i < n && j < n) v = Q[(b * n + i) * n + j] + (i == j ? sigma : 0.f);
-    else if (i < n) v = A0[(b * m + (j - n)) * n + i];
-    else if (j < n) v = A0[(b * m + (i - n)) * n + j];
+    if (i < n && j < n) v = Qb[(size_t)i * n + j] + (i == j ? sigma : 0.f);
+    else if (i < n) v = T[jj][ii];
+    else if (j < n) v = Ab[(size_t)(i - n) * n + j];
     else if (i != j) v = -0.f;
     else if (rho_rows) v = -(1.0f / rho_rows[b * m + (i - n)]);
     else v = -((i - n) < num_ineq ? irho_in : irho_eq);
-    K[k] = v;
+    Kb[(size_t)i * N + j] = v;
   }
 }
 
@@ -407,10 +422,10 @@ extern "C" int iadmm_kkt_assemble(int64_t B, int64_t n, int64_t m, int64_t num_i
   if (B <= 0 || n <= 0 || m < 0 || num_ineq < 0 || num_ineq > m || !Q || !K || (m > 0 && !A0))
     return IADMM_E_ARG;
   if (m > 0 && !scal && !rho_rows) return IADMM_E_ARG;
-  const int64_t tot = B * (n + m) * (n + m);
-  const int64_t blocks = (tot + 255) / 256;
-  hipLaunchKernelGGL(kkt_assemble_kernel, dim3((unsigned)(blocks < 16384 ? blocks : 16384)), dim3(256), 0,
-                     (hipStream_t)stream, B, (int)n, (int)m, (int)num_ineq, Q, A0, sigma, scal, rho_rows, K);
+  const int64_t ntile = (n + m + kAsmT - 1) / kAsmT;
+  if (B > 0x7fffffff || ntile * ntile > 65535) return IADMM_E_SIZE;
+  hipLaunchKernelGGL(kkt_assemble_kernel, dim3((unsigned)B, (unsigned)(ntile * ntile)), dim3(256), 0,
+                     (hipStream_t)stream, (int)n, (int)m, (int)num_ineq, (int)ntile, Q, A0, sigma, scal, rho_rows, K);
   IADMM_CHECK_LAUNCH();
   return 0;
 }
