@@ -539,33 +539,51 @@ __global__ __launch_bounds__(kSolveThreads) void lu_solve_kernel(int N, const fl
         const int r = idx / nbk, c = idx % nbk;
         D[r * kDS + c] = M[(size_t)(k0 + r) * N + k0 + c];
       }
-      for (int i = wave; i < nbk; i += nw) {  // prefix (forward) / suffix (backward) dot products
-        const float* row = M + (size_t)(k0 + i) * N;
-        const int j0 = pass == 0 ? 0 : k1, j1 = pass == 0 ? k0 : N;
-        float d = 0.f;
-        if constexpr (VEC) {
-          // 16-B loads, 4 in flight per lane: a latency-bound scalar stream ran at ~2 TB/s
-          const float4* r4 = reinterpret_cast<const float4*>(row);
-          const float4* x4 = reinterpret_cast<const float4*>(x);
-          const int q1 = j1 >> 2;
-          int q = (j0 >> 2) + lane;
-          for (; q + 192 < q1; q += 256) {
-            const float4 a0 = r4[q], a1 = r4[q + 64], a2 = r4[q + 128], a3 = r4[q + 192];
-            const float4 b0 = x4[q], b1 = x4[q + 64], b2 = x4[q + 128], b3 = x4[q + 192];
-            d = fmaf(a0.x, b0.x, d); d = fmaf(a0.y, b0.y, d); d = fmaf(a0.z, b0.z, d); d = fmaf(a0.w, b0.w, d);
-            d = fmaf(a1.x, b1.x, d); d = fmaf(a1.y, b1.y, d); d = fmaf(a1.z, b1.z, d); d = fmaf(a1.w, b1.w, d);
-            d = fmaf(a2.x, b2.x, d); d = fmaf(a2.y, b2.y, d); d = fmaf(a2.z, b2.z, d); d = fmaf(a2.w, b2.w, d);
-            d = fmaf(a3.x, b3.x, d); d = fmaf(a3.y, b3.y, d); d = fmaf(a3.z, b3.z, d); d = fmaf(a3.w, b3.w, d);
+      // prefix (forward) / suffix (backward) dot products of the block rows with x: all rows of a
+      // block share the column range, so a wave takes 4 rows at a time (16-B loads, 8 in flight
+      // per lane, x read once for the 4): one memory latency per 4 rows instead of per row.
+      const int j0 = pass == 0 ? 0 : k1, j1 = pass == 0 ? k0 : N;
+      if constexpr (VEC) {
+        const float4* x4 = reinterpret_cast<const float4*>(x);
+        const int q0 = j0 >> 2, q1 = j1 >> 2;
+        for (int g = wave * 4; g < nbk; g += nw * 4) {
+          const float4* r4[4];
+#pragma unroll
+          for (int rr = 0; rr < 4; ++rr)
+            r4[rr] = reinterpret_cast<const float4*>(M + (size_t)(k0 + min(g + rr, nbk - 1)) * N);
+          float d[4] = {0.f, 0.f, 0.f, 0.f};
+          auto dot4 = [](const float4& u, const float4& w, float acc) {
+            acc = fmaf(u.x, w.x, acc); acc = fmaf(u.y, w.y, acc);
+            acc = fmaf(u.z, w.z, acc); return fmaf(u.w, w.w, acc);
+          };
+          int q = q0 + lane;
+          for (; q + 64 < q1; q += 128) {
+            const float4 b0 = x4[q], b1 = x4[q + 64];
+            float4 a0[4], a1[4];
+#pragma unroll
+            for (int rr = 0; rr < 4; ++rr) { a0[rr] = r4[rr][q]; a1[rr] = r4[rr][q + 64]; }
+#pragma unroll
+            for (int rr = 0; rr < 4; ++rr) d[rr] = dot4(a1[rr], b1, dot4(a0[rr], b0, d[rr]));
           }
-          for (; q < q1; q += 64) {
-            const float4 a0 = r4[q], b0 = x4[q];
-            d = fmaf(a0.x, b0.x, d); d = fmaf(a0.y, b0.y, d); d = fmaf(a0.z, b0.z, d); d = fmaf(a0.w, b0.w, d);
+          if (q < q1) {
+            const float4 b0 = x4[q];
+#pragma unroll
+            for (int rr = 0; rr < 4; ++rr) d[rr] = dot4(r4[rr][q], b0, d[rr]);
           }
-        } else {
-          for (int j = j0 + lane; j < j1; j += 64) d = fmaf(row[j], x[j], d);
+#pragma unroll
+          for (int rr = 0; rr < 4; ++rr) {
+            const float t = wave_sum(d[rr]);
+            if (lane == 0 && g + rr < nbk) s[g + rr] = t;
+          }
         }
-        d = wave_sum(d);
-        if (lane == 0) s[i] = d;
+      } else {
+        for (int i = wave; i < nbk; i += nw) {
+          const float* row = M + (size_t)(k0 + i) * N;
+          float d = 0.f;
+          for (int j = j0 + lane; j < j1; j += 64) d = fmaf(row[j], x[j], d);
+          d = wave_sum(d);
+          if (lane == 0) s[i] = d;
+        }
       }
       __syncthreads();
       if (wave == 0) {
