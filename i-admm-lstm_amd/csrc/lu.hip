@@ -127,74 +127,74 @@ __global__ __launch_bounds__(kLuThreads, 2) void lu_panel_kernel(int N, int K0, 
 #pragma unroll
   for (int j = 0; j < kNB; ++j) {
     if (j < nb) {
-    float best = -1.f;
-    int bi = R;
-#pragma unroll
-    for (int m = 0; m < M; ++m) {
-      const int r = tid + kLuThreads * m;
-      const float v = fabsf(col_of(a[m], j));
-      if (r >= j && r < R && v > best) { best = v; bi = r; }
-    }
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) {
-      const float ov = __shfl_xor(best, o, 64);
-      const int oi = __shfl_xor(bi, o, 64);
-      if (ov > best || (ov == best && oi < bi)) { best = ov; bi = oi; }
-    }
-    if (lane == 0) { rv[wave] = best; ri[wave] = bi; }
-    if (tid == j) {
-#pragma unroll
-      for (int c = 0; c < kNB; ++c) xrow[0][c] = a[0][c];
-    }
-    __syncthreads();
-    if (tid == 0) {
-      float bv = rv[0];
-      int bx = ri[0];
-      for (int w = 1; w < kLuThreads / 64; ++w)
-        if (rv[w] > bv || (rv[w] == bv && ri[w] < bx)) { bv = rv[w]; bx = ri[w]; }
-      if (bx >= R) bx = j;  // all entries NaN: keep the diagonal
-      else if (bv == 0.f && info[b] == 0) info[b] = k0 + j + 1;
-      ri[4] = bx;
-      piv[b * N + k0 + j] = k0 + bx;
-      pvs[j] = k0 + bx;
-    }
-    __syncthreads();
-    const int p = ri[4];
-    // the owner of row p publishes it and takes row j's values
-#pragma unroll
-    for (int m = 0; m < M; ++m)
-      if (tid + kLuThreads * m == p) {
-#pragma unroll
-        for (int c = 0; c < kNB; ++c) {
-          xrow[1][c] = a[m][c];
-          a[m][c] = xrow[0][c];
-        }
-      }
-    __syncthreads();
-    if (tid == j) {
-#pragma unroll
-      for (int c = 0; c < kNB; ++c) a[0][c] = xrow[1][c];
-    }
-    const float pv = xrow[1][j];
-    if (pv != 0.f) {
-      const float rcp = 1.0f / pv;
-      float pr[kNB];
-#pragma unroll
-      for (int c = 0; c < kNB; ++c) pr[c] = xrow[1][c];
+      float best = -1.f;
+      int bi = R;
 #pragma unroll
       for (int m = 0; m < M; ++m) {
         const int r = tid + kLuThreads * m;
-        if (r > j && r < R) {
-          const float l = col_of(a[m], j) * rcp;
+        const float v = fabsf(col_of(a[m], j));
+        if (r >= j && r < R && v > best) { best = v; bi = r; }
+      }
 #pragma unroll
-          for (int c = 0; c < kNB; ++c) {  // static register indices: j is not a compile-time constant
-            if (c == j) a[m][c] = l;
-            else if (c > j) a[m][c] = a[m][c] - l * pr[c];
+      for (int o = 32; o >= 1; o >>= 1) {
+        const float ov = __shfl_xor(best, o, 64);
+        const int oi = __shfl_xor(bi, o, 64);
+        if (ov > best || (ov == best && oi < bi)) { best = ov; bi = oi; }
+      }
+      if (lane == 0) { rv[wave] = best; ri[wave] = bi; }
+      if (tid == j) {
+#pragma unroll
+        for (int c = 0; c < kNB; ++c) xrow[0][c] = a[0][c];
+      }
+      __syncthreads();
+      if (tid == 0) {
+        float bv = rv[0];
+        int bx = ri[0];
+        for (int w = 1; w < kLuThreads / 64; ++w)
+          if (rv[w] > bv || (rv[w] == bv && ri[w] < bx)) { bv = rv[w]; bx = ri[w]; }
+        if (bx >= R) bx = j;  // all entries NaN: keep the diagonal
+        else if (bv == 0.f && info[b] == 0) info[b] = k0 + j + 1;
+        ri[4] = bx;
+        piv[b * N + k0 + j] = k0 + bx;
+        pvs[j] = k0 + bx;
+      }
+      __syncthreads();
+      const int p = ri[4];
+      // the owner of row p publishes it and takes row j's values
+#pragma unroll
+      for (int m = 0; m < M; ++m)
+        if (tid + kLuThreads * m == p) {
+#pragma unroll
+          for (int c = 0; c < kNB; ++c) {
+            xrow[1][c] = a[m][c];
+            a[m][c] = xrow[0][c];
+          }
+        }
+      __syncthreads();
+      if (tid == j) {
+#pragma unroll
+        for (int c = 0; c < kNB; ++c) a[0][c] = xrow[1][c];
+      }
+      const float pv = xrow[1][j];
+      if (pv != 0.f) {
+        const float rcp = 1.0f / pv;
+        float pr[kNB];
+#pragma unroll
+        for (int c = 0; c < kNB; ++c) pr[c] = xrow[1][c];
+#pragma unroll
+        for (int m = 0; m < M; ++m) {
+          const int r = tid + kLuThreads * m;
+          if (r > j && r < R) {
+            const float l = col_of(a[m], j) * rcp;
+#pragma unroll
+            for (int c = 0; c < kNB; ++c) {  // static register indices: j is not a compile-time constant
+              if (c == j) a[m][c] = l;
+              else if (c > j) a[m][c] = a[m][c] - l * pr[c];
+            }
           }
         }
       }
-    }
-    __syncthreads();  // xrow is rewritten by the next column
+      __syncthreads();  // xrow is rewritten by the next column
     }
   }
 

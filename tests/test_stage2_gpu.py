@@ -26,9 +26,11 @@ def _gpu():
         pytest.skip("no GPU")
 
 
-# 16 / 37 / 64: one 64-column block; 100, 130, 257 (N % 4 != 0: scalar trailing-update loads),
-# 400, 2000: several blocks with partial 128 x 128 trailing tiles
-@pytest.mark.parametrize("N,B", [(16, 2), (37, 3), (64, 2), (100, 2), (130, 2), (257, 2), (400, 2), (2000, 1)])
+# 16 / 37 / 64: one 64-column block (single-row-slot panels); 100, 130, 257, 1101 (N % 4 != 0:
+# scalar trailing-update accesses; 1101 also two 1024-row trailing chunks and 4- and 8-slot
+# panels); 400, 2000: several blocks with partial 128-column strips and 64-row steps
+@pytest.mark.parametrize("N,B", [(16, 2), (37, 3), (64, 2), (100, 2), (130, 2), (257, 2), (400, 2), (1101, 1),
+                                 (2000, 1)])
 def test_lu_factor_solve_backward_error(N, B):
     from iadmm import ops
     g = torch.Generator().manual_seed(N)
