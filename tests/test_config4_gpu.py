@@ -18,6 +18,7 @@ def rel_l2(a, b):
     return float((a - b).norm() / max(b.norm(), 1e-30))
 
 
+@pytest.mark.timeout(900)  # the CPU oracle at n + m = 10000, h = 2048 alone takes minutes on a busy host
 def test_config4_shape_vs_oracle():
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
