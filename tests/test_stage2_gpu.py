@@ -47,11 +47,12 @@ def test_lu_factor_solve_backward_error(N, B):
     assert (piv[:, 0].cpu() != 0).all()
 
 
-def test_lu_pivots_match_lapack_choice():
+@pytest.mark.parametrize("N", [48, 300])  # one 64-column block; several (deferred block interchanges)
+def test_lu_pivots_match_lapack_choice(N):
     """Same pivot sequence as partial pivoting with first-max tie-breaking (LAPACK i?amax)."""
     from iadmm import ops
     g = torch.Generator().manual_seed(7)
-    K = torch.randn(2, 48, 48, generator=g)
+    K = torch.randn(2, N, N, generator=g)
     _, piv, _ = ops.lu_factor(K.cuda().contiguous())
     torch.set_num_threads(1)
     _, ref = torch.linalg.lu_factor(K.double())
