@@ -53,10 +53,12 @@ def test_lu_pivots_match_lapack_choice(N):
     from iadmm import ops
     g = torch.Generator().manual_seed(7)
     K = torch.randn(2, N, N, generator=g)
-    _, piv, _ = ops.lu_factor(K.cuda().contiguous())
+    LU, piv, _ = ops.lu_factor(K.cuda().contiguous())
     torch.set_num_threads(1)
-    _, ref = torch.linalg.lu_factor(K.double())
+    lu_ref, ref = torch.linalg.lu_factor(K.double())
     assert torch.equal(piv.cpu().long(), ref.long() - 1)
+    # same pivots -> the same factors up to fp32 rounding growth (L and U packed like LAPACK's)
+    assert rel_l2(LU, lu_ref) < 1e-5
 
 
 def test_lu_singular_reports_info():
