@@ -3,8 +3,11 @@
 A "step" = one full test-mode solve of the per-GPU batch, already resident in HBM (the timed
 scope of main.py:825-834,881-890,1024-1031): Ruiz scaling (10 rounds) -> K=100 Stage-I
 iterations -> final unscale.  Instances: n=1000, 500 inequality + 500 equality rows, hidden 800,
-B=1024 per GPU (synthetic, restating generate_data.py:67-76; random-init weights with the
-reference's initialisation — throughput does not depend on weight values).
+B=1024 per GPU (synthetic, restating generate_data.py:67-76).  Weights: the checkpoint
+``checkpoints/QP_{n}_{eq}_{ineq}_{T}_{h}.pth`` (trained by tools/train_checkpoint.py with this
+repo's HIP training path; main.py's naming) when it exists, else random init with the reference's
+initialisation.  Throughput does not depend on weight values; the final residual does (the
+random-init solve diverges at this shape), so both are reported when a checkpoint is used.
 
 Multi-GPU: one process per GPU (torch.distributed.run); the instance batch is sharded (rank r
 solves instances [r*B, (r+1)*B)) with no data-path collective; a barrier brackets the timed
@@ -15,7 +18,9 @@ Prints ONE JSON line on rank 0, including
                 every launch inside the timed region, plus the same for the HBM-bound residual
                 matvec (iadmm_kkt_resgrad) under "roofline_matvec";
   cpu_baseline  the CPU oracle (oracle/iadmm_oracle.py: the reference's op structure in
-                PyTorch-CPU fp32) on a bounded sample of the same workload, rank 0 only.
+                PyTorch-CPU fp32) on a bounded sample of the same workload, rank 0 only, with
+                a parity block: the GPU's result on the SAME instances against the oracle's
+                (x, y, z rel-L2, primal/dual relative error, K = outer_T iterations).
 """
 import argparse
 import json
@@ -45,7 +50,13 @@ def parse():
     ap.add_argument("--hidden_dim", type=int, default=800)
     ap.add_argument("--outer_T", type=int, default=100)
     ap.add_argument("--sigma", type=float, default=6e-6)
-    ap.add_argument("--cpu-sample", type=int, default=8, help="instances in the CPU baseline (0: skip)")
+    ap.add_argument("--cpu-sample", type=int, default=8,
+                    help="instances in the CPU baseline (0: skip).  8 of config 1's 64: the CPU cost is "
+                         "linear in the batch (batched ops, no cross-instance work), and 64 would take "
+                         "~4 min of CPU time, beyond the bench's bounded-sample budget")
+    ap.add_argument("--weights", type=str, default="auto",
+                    help="'auto' (the checkpoint under checkpoints/ when present, else random init), "
+                         "'random', or a .pth path")
     ap.add_argument("--alt-f16x3", type=int, default=1,
                     help="also time one step of the optional split-precision cell (reported under "
                          "'alt_precision', never as the headline value)")
@@ -87,23 +98,95 @@ def baseline_config(args, world):
     return "custom shape"
 
 
-def cpu_baseline(args, d, params):
-    """Oracle (reference op structure, torch-CPU fp32) on the first ``cpu_sample`` instances."""
+def cpu_model():
+    """Host CPU model name (/proc/cpuinfo), for the cpu_baseline record."""
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    import platform
+    return platform.processor() or "unknown"
+
+
+PARITY_TOL = {"x": 1e-4, "z": 1e-4, "y": 5e-3, "primal": 1e-4, "dual": 1e-4}
+"""Stated fp32 tolerance of the GPU-vs-oracle comparison (SURVEY.md §8(c) contract: rel-L2(x^K)
+and primal/dual relative error <= 1e-4; y <= 5e-3 because the equality-row update
+y = rho_eq (z~ - b) with rho_eq ~ 500 cancels ~3 digits, DESIGN.md §4).  Divergent dynamics
+(random-init weights at this shape) amplify rounding differences, so that regime is reported
+but not held to the tolerance."""
+
+
+def parity(gpu, ref, Bc):
+    """GPU result of instances [0, Bc) against the oracle's on the same instances."""
+    res = {}
+    for k in ("x", "y", "z"):
+        a = gpu[k][:Bc].reshape(Bc, -1).double().cpu()
+        b = ref[k].reshape(Bc, -1).double()
+        res[k + "_rel_l2"] = float(((a - b).norm(dim=1) / b.norm(dim=1).clamp_min(1e-30)).max())
+    for k in ("primal", "dual"):
+        a = gpu[k][:Bc].reshape(-1).double().cpu()
+        b = ref[k].reshape(-1).double()
+        res[k + "_max_rel"] = float(((a - b).abs() / b.abs().clamp_min(1e-30)).max())
+        res[k + "_mean_gpu"] = float(a.mean())
+        res[k + "_mean_cpu"] = float(b.mean())
+    res["tol"] = PARITY_TOL
+    res["within_tol"] = all(res[k + ("_rel_l2" if k in "xyz" else "_max_rel")] <= v for k, v in PARITY_TOL.items())
+    return res
+
+
+def run_oracle(args, cpu, params):
     from oracle import iadmm_oracle as orc
-    Bc = args.cpu_sample
-    threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
-    torch.set_num_threads(threads)
-    cpu = {k: d[k][:Bc].cpu() for k in ("Q", "p", "A0", "zl", "zu")}
     pc = {k: v.detach().cpu() for k, v in params.items()}
     t0 = time.perf_counter()
     with torch.no_grad():
         out = orc.solve(pc, cpu["Q"], cpu["p"], cpu["A0"], cpu["zl"], cpu["zu"], args.num_ineq, args.num_eq,
                         args.outer_T, args.sigma, args.hidden_dim)
-    dt = time.perf_counter() - t0
-    return dict(value=Bc / dt, unit="QP instances/s", cores=threads, kind="port",
-                sample=f"{Bc} instances x full solve (Ruiz + K={args.outer_T} + unscale), same synthetic "
-                       f"instances and weights as the GPU run, {dt:.1f} s",
-                final_primal=float(out["primal"].mean()), final_dual=float(out["dual"].mean()))
+    return out, time.perf_counter() - t0
+
+
+def cpu_baseline(args, d, params, gpu_out, weights_tag, extra=()):
+    """Oracle (reference op structure, torch-CPU fp32) on the first ``cpu_sample`` instances, timed
+    (the baseline) and compared with the GPU's result on the same instances (parity).  ``extra``:
+    further (tag, params, gpu_out) sets checked for parity only (untimed)."""
+    Bc = args.cpu_sample
+    threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+    torch.set_num_threads(threads)
+    cpu = {k: d[k][:Bc].cpu() for k in ("Q", "p", "A0", "zl", "zu")}
+    out, dt = run_oracle(args, cpu, params)
+    rec = dict(value=Bc / dt, unit="QP instances/s", cores=threads, kind="port", cpu_model=cpu_model(),
+               sample=f"{Bc} instances x full solve (Ruiz + K={args.outer_T} + unscale), the same synthetic "
+                      f"instances 0..{Bc - 1} and weights ({weights_tag}) as the GPU run, {dt:.1f} s; "
+                      f"8 of config 1's 64 instances (CPU cost is linear in the batch)",
+               final_primal=float(out["primal"].mean()), final_dual=float(out["dual"].mean()),
+               parity={weights_tag: parity(gpu_out, out, Bc)})
+    for tag, prm, gout in extra:
+        o, _ = run_oracle(args, cpu, prm)
+        rec["parity"][tag] = parity(gout, o, Bc)
+    return rec
+
+
+def load_weights(args, h, T):
+    """(params dict on cuda, tag): the checkpoint named like main.py's (QP_{n}_{eq}_{ineq}_{T}_{h})
+    under checkpoints/ for --weights auto, a given .pth, or random init."""
+    from iadmm import data
+    from iadmm.solver import PARAM_NAMES
+    path = None
+    if args.weights == "auto":
+        cand = os.path.join(ROOT, "checkpoints", f"QP_{args.num_var}_{args.num_eq}_{args.num_ineq}_{T}_{h}.pth")
+        path = cand if os.path.exists(cand) else None
+    elif args.weights != "random":
+        path = args.weights
+    if path is None:
+        return data.init_lstm_params(h, T, device="cuda"), "random-init"
+    sd = torch.load(path, map_location="cuda", weights_only=True)
+    params = {k: sd[k].float().contiguous() for k in PARAM_NAMES}
+    if params["U_i"].shape[0] != h or params["rho"].shape[0] < T:
+        raise SystemExit(f"{path}: hidden {params['U_i'].shape[0]} / length {params['rho'].shape[0]} "
+                         f"do not fit hidden_dim={h}, outer_T={T}")
+    return params, "trained:" + os.path.relpath(path, ROOT)
 
 
 def heartbeat(period_s=60.0):
@@ -133,7 +216,7 @@ def main():
     N = n + mi + me
     first, count = parallel.shard(world * B, world, rank)  # weak scaling: B instances per GPU
     d = data.make_qp_batch(n, mi, me, count, first_index=first, device="cuda")
-    params = data.init_lstm_params(h, T, device="cuda")
+    params, weights_tag = load_weights(args, h, T)
     packed = solver.PackedWeights()
     keep = not args.in_place_scaling
     if not keep and args.warmup + args.steps > 1:
@@ -144,14 +227,14 @@ def main():
     elif not keep:
         master = None
 
-    def step(timer, precision="f32"):
+    def step(timer, precision="f32", prm=None):
         if not keep and master is not None:
             for k in d:
                 d[k].copy_(master[k])
             torch.cuda.synchronize()
         with torch.no_grad():
-            return solver.solve(params, d["Q"], d["p"], d["A0"], d["zl"], d["zu"], mi, me, T, args.sigma,
-                                keep_unscaled=keep, packed=packed, timer=timer, precision=precision)
+            return solver.solve(prm or params, d["Q"], d["p"], d["A0"], d["zl"], d["zu"], mi, me, T, args.sigma,
+                                keep_unscaled=keep, packed=None if prm else packed, timer=timer, precision=precision)
 
     for _ in range(args.warmup):
         step(None)
@@ -207,6 +290,14 @@ def main():
                "x_rel_l2_vs_f32_run": float((out16["x"] - x32).norm() / x32.norm().clamp_min(1e-30))}
         del out16
 
+    # the random-init weights' residual beside the trained one (untimed: same work, other values)
+    rand = None
+    if weights_tag != "random-init" and (keep or master is not None):
+        prm_r = data.init_lstm_params(h, T, device="cuda")
+        out_r = step(None, prm=prm_r)
+        rand = (prm_r, {k: out_r[k] for k in ("x", "y", "z", "primal", "dual")})
+        del out_r
+
     res = None
     if rank == 0:
         total = world * B * args.steps
@@ -222,13 +313,14 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f32",
-            "data": "synthetic (generate_data.py:67-76 distribution, per-instance seeds; random-init weights)",
+            "data": f"synthetic (generate_data.py:67-76 distribution, per-instance seeds); weights {weights_tag}",
             "config": {"workload": f"QP n={n} ineq={mi} eq={me} K={T} hidden={h} --test --scaling, "
                                    f"batch={B}/GPU ({baseline_config(args, world)})",
                        "global_batch": world * B, "num_var": n, "num_ineq": mi, "num_eq": me,
                        "outer_T": T, "hidden_dim": h, "parallelism": f"instance-shard x{world}",
                        "in_place_scaling": not keep},
-            "final_residual": {"primal_mean": primal, "dual_mean": dual, "sum": primal + dual},
+            "final_residual": {"primal_mean": primal, "dual_mean": dual, "sum": primal + dual,
+                               "weights": weights_tag},
             "roofline": {"kernel": "iadmm_lstm_cell_fwd", "bound": "mfma", "achieved": cell_tf,
                          "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": cell_tf / FP32_MFMA_PEAK_TFLOPS,
                          "traffic": pmc_traffic(("cell_fwd_dma_kernel",), n, mi + me, h, B),
@@ -244,8 +336,12 @@ def main():
         }
         if alt is not None:
             res["alt_precision"] = alt
+        if rand is not None:
+            pr_r, du_r = float(rand[1]["primal"].mean()), float(rand[1]["dual"].mean())
+            res["final_residual_random_init"] = {"primal_mean": pr_r, "dual_mean": du_r, "sum": pr_r + du_r}
         if args.cpu_sample > 0 and world == 1:  # the CPU baseline is an N=1 figure
-            res["cpu_baseline"] = cpu_baseline(args, d if keep else master, params)
+            extra = [("random-init", rand[0], rand[1])] if rand is not None else []
+            res["cpu_baseline"] = cpu_baseline(args, d if keep else master, params, out, weights_tag, extra)
         print(json.dumps(res), flush=True)
     if dist:
         dist.barrier()

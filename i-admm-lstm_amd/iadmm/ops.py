@@ -250,9 +250,16 @@ def lu_factor(K):
 def lu_solve(LU, piv, b):
     """Solve with (LU, piv) in place on a copy of b [B,N]; returns x."""
     B, N = LU.shape[0], LU.shape[1]
-    x = b.clone().contiguous()
+    if LU.dim() != 3 or LU.shape[2] != N:
+        raise ValueError(f"LU must be [B,N,N], got {tuple(LU.shape)}")
     if piv.dtype != torch.int32 or not piv.is_contiguous():
         raise TypeError("piv must be contiguous int32")
+    if not piv.is_cuda or piv.device != LU.device:
+        raise ValueError("piv must be on the device of LU")
+    if tuple(piv.shape) != (B, N) or b.numel() != B * N:
+        raise ValueError(f"piv must be [B,N] = [{B},{N}] and b hold B*N values; got piv {tuple(piv.shape)}, "
+                         f"b {tuple(b.shape)}")
+    x = b.clone().contiguous()
     _abi.call("iadmm_lu_solve", B, N, _p(LU), piv.data_ptr(), _p(x), _stream())
     return x
 

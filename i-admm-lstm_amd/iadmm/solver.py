@@ -174,9 +174,13 @@ def solve(params, Q, p, A0, zl, zu, num_ineq, num_eq, T, sigma, scaling=True, sc
         tmp = (torch.empty(B, n, **f32), torch.empty(B, m, **f32), torch.empty(B, m, **f32))
 
     cur = 0
-    tok = timer.start("iterations")
+    # timed scope = the reference's model() calls (main.py:881-890): with history the per-iteration
+    # metric work runs in "hist:" spans that the CLI's Parallel Time leaves out
+    tok = timer.start("iterations") if not history else None
     for t in range(T):
         nxt = 1 - cur
+        if history:
+            tok = timer.start("iterations")
         ops.schedule(rho_p, alpha_p, t, out=scal)
         k = timer.start("k:kkt_resgrad")
         ops.kkt_resgrad(Qs, As, pv, xs[cur], ys[cur], zs[cur], xvs[cur], sigma, scal, num_ineq, g=g)
@@ -191,6 +195,8 @@ def solve(params, Q, p, A0, zl, zu, num_ineq, num_eq, T, sigma, scaling=True, sc
         ops.admm_update(n, m, num_ineq, part, b_h, xvs[cur], xs[cur], ys[cur], zs[cur], zlv, zuv, scal,
                         out=(xvs[nxt], xs[nxt], ys[nxt], zs[nxt]))
         if history:  # main.py:949-957 on unscaled data; kept on device
+            timer.stop(tok)
+            htok = timer.start("hist:metrics")
             ops.kkt_lsres(Qs, As, pv, xs[cur], ys[cur], zs[cur], xvs[nxt], sigma, scal, num_ineq,
                           out=hist[1, t])
             if scaling:
@@ -204,8 +210,10 @@ def solve(params, Q, p, A0, zl, zu, num_ineq, num_eq, T, sigma, scaling=True, sc
             hist[3, t].copy_(du)
             if iter_hook is not None:  # extra per-iteration device metrics (main.py:959-978)
                 iter_hook(t, ux, uy, uz)
+            timer.stop(htok)
         cur = nxt
-    timer.stop(tok)
+    if not history:
+        timer.stop(tok)
 
     tok = timer.start("unscale")
     if scaling:
@@ -266,12 +274,16 @@ def fixed_alpha_scal(alpha, device):
     return s.to(device)
 
 
-def stage2(Q, p, A0, zl, zu, rho_rows, x, y, z, sigma, iters, alpha=STAGE2_ALPHA, timer=None, iter_hook=None):
+def stage2(Q, p, A0, zl, zu, rho_rows, x, y, z, sigma, iters, alpha=STAGE2_ALPHA, timer=None, iter_hook=None,
+           history=False):
     """Stage II feasibility restoration (models/lu.py:13-47, driver main.py:1035-1066):
     factor K once (rho of the last Stage-I iteration), then ``iters`` exact ADMM steps with
     alpha-relaxation on x and z.  Works on the unscaled data like the reference.
     Q[B,n,n], p[B,n], A0[B,m,n], zl/zu/rho_rows[B,m], x[B,n], y/z[B,m].  Returns the iterates and
-    the factors (LU, piv).  ``iter_hook(t, x, y, z)`` runs after every iteration (metrics)."""
+    the factors (LU, piv).  A singular K raises (like models/lu.py's torch.lu check).
+    ``history=True`` records per-iteration obj / ls_res / primal / dual [4, iters, B] on the device
+    (main.py:1068-1076: ls_res = ||K xv - b~|| with the solve's own K and b~) and
+    ``iter_hook(t, x, y, z)`` runs after every iteration; both in "hist:" timer spans."""
     timer = timer or Timer(False)
     B, n = x.shape
     m = y.shape[1]
@@ -280,14 +292,31 @@ def stage2(Q, p, A0, zl, zu, rho_rows, x, y, z, sigma, iters, alpha=STAGE2_ALPHA
     K = ops.kkt_assemble(Q, A0, sigma, None, 0, rho_rows=rho_rows)
     LU, piv, info = ops.lu_factor(K)
     timer.stop(tok)
-    tok = timer.start("stage2_iterations")
+    bad = int(info.max())  # one host read per factorisation
+    if bad:
+        raise RuntimeError(f"Stage II LU: U({bad},{bad}) is exactly zero (singular KKT matrix)")
+    hist = torch.zeros(4, iters, B, dtype=torch.float32, device=x.device) if history else None
     xv = None
-    for _ in range(iters):
+    for t in range(iters):
+        tok = timer.start("stage2_iterations")
         b = ops.kkt_rhs(p, x, y, z, sigma, rho_rows=rho_rows)
         xs = ops.lu_solve(LU, piv, b)
         xv, x, y, z = ops.admm_update(n, m, 0, None, None, xs, x, y, z, zl, zu, scal, relax_z=True,
                                       rho_rows=rho_rows)
-        if iter_hook is not None:
-            iter_hook(_, x, y, z)
-    timer.stop(tok)
-    return dict(x=x, y=y, z=z, xv=xv, LU=LU, piv=piv, info=info)
+        timer.stop(tok)
+        if history or iter_hook is not None:
+            htok = timer.start("hist:stage2")
+            if history:
+                r = ops.kkt_matvec(Q, A0, xv, sigma, None, 0, rho_rows=rho_rows) - b
+                hist[1, t].copy_(r.norm(dim=1))
+                o, pr, du = ops.metrics(Q, p, A0, x, y, z)
+                hist[0, t].copy_(o)
+                hist[2, t].copy_(pr)
+                hist[3, t].copy_(du)
+            if iter_hook is not None:
+                iter_hook(t, x, y, z)
+            timer.stop(htok)
+    out = dict(x=x, y=y, z=z, xv=xv, LU=LU, piv=piv, info=info)
+    if history:
+        out.update(hist_obj=hist[0], hist_ls_res=hist[1], hist_primal=hist[2], hist_dual=hist[3])
+    return out

@@ -49,12 +49,14 @@ def allreduce_grads(params, dist, bucket_bytes=32 << 20):
 
 
 def tbptt_batch(model, data, num_ineq, num_eq, outer_T, truncated_length, sigma, optimizer,
-                micro_batch=None, global_batch=None, dist=None, loss_fn=None):
+                micro_batch=None, global_batch=None, dist=None, loss_fn=None, final=None):
     """Train on one (already scaled) batch: ``outer_T // truncated_length`` windows, each ending
     in one optimiser step, like main.py:336-358 (t restarts at 0 in every window, as there).
 
     ``data`` = dict(Q, p, A0, zl, zu) of this rank's instances; ``global_batch`` = instances over
-    all ranks (default: this rank's).  Returns the mean training loss of the last window."""
+    all ranks (default: this rank's).  Returns the mean training loss of the last window; a dict
+    passed as ``final`` receives this rank's last (scaled) iterate x [B,n,1] (the epoch report's
+    Train_Obj / violations, main.py:362-379)."""
     if loss_fn is None:
         import utils
         loss_fn = utils.primal_dual_loss
@@ -93,6 +95,8 @@ def tbptt_batch(model, data, num_ineq, num_eq, outer_T, truncated_length, sigma,
             dist.all_reduce(window_loss)
         optimizer.step()
         last = float(window_loss)
+    if final is not None:
+        final["x"] = torch.cat([states[s][0] for s, _ in chunks])
     return last
 
 

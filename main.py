@@ -165,16 +165,14 @@ def run_test(args):
                                scaling=args.scaling, scaling_iters=args.scaling_ites, history=True,
                                packed=packed, timer=timer, iter_hook=hook)
             spans = timer.totals_ms()
-            total_time += sum(v for k, v in spans.items() if not k.startswith("k:")) / 1e3
+            total_time += timed_seconds(spans)
             h = {k: out["hist_" + k].mean(1).cpu().numpy() for k in ("obj", "ls_res", "primal", "dual")}
             h["viol"] = viol.mean(2).cpu().numpy()
             if args.feas_rest:  # Stage II on the unscaled data with the last rho (main.py:1035-1066)
                 F = args.feas_rest_num
-                fobj = torch.zeros(F, tb, device=device)
                 fvio = torch.zeros(4, F, tb, device=device)
 
                 def fhook(t, x, y, z):
-                    fobj[t] = ops.metrics(d["Q"], d["p"].reshape(tb, -1), d["A0"], x, y, z)[0]
                     if mi:
                         iv = ops.bmv(G, x, c, ops.BMV_POS_EXCESS)
                         fvio[0, t], fvio[1, t] = iv.max(1).values, iv.mean(1)
@@ -187,9 +185,10 @@ def run_test(args):
                 s2 = solver.stage2(d["Q"], d["p"].reshape(tb, -1).contiguous(), d["A0"], d["zl"].reshape(tb, -1).contiguous(),
                                    d["zu"].reshape(tb, -1).contiguous(), rho_rows, out["x"].reshape(tb, -1).contiguous(),
                                    out["y"].reshape(tb, -1).contiguous(), out["z"].reshape(tb, -1).contiguous(),
-                                   args.sigma, F, timer=ftimer, iter_hook=fhook)
-                total_time += sum(ftimer.totals_ms().values()) / 1e3
-                h["fr_obj"] = fobj.mean(1).cpu().numpy()
+                                   args.sigma, F, timer=ftimer, iter_hook=fhook, history=True)
+                total_time += timed_seconds(ftimer.totals_ms())
+                for k in ("obj", "ls_res", "primal", "dual"):
+                    h["fr_" + k] = s2["hist_" + k].mean(1).cpu().numpy()
                 h["fr_viol"] = fvio.mean(2).cpu().numpy()
                 out["x"] = s2["x"].unsqueeze(-1)
             reports.append(h)
@@ -205,7 +204,7 @@ def run_test(args):
             print("Test_Max_Eq : {:.3f} | Test_Mean_Eq : {:.3f} |".format(vi[2, t], vi[3, t]))
     if args.feas_rest:  # main.py:1140-1161
         print("-----Starting Sage II-----")
-        fr = np.mean([r["fr_obj"] for r in reports], axis=0)
+        fr = mean("fr_obj")
         fv = np.mean([r["fr_viol"] for r in reports], axis=0)
         for t in range(args.feas_rest_num):
             print("Epoch : {} | Test_Obj : {:.3f}".format(t, fr[t]))
@@ -219,12 +218,44 @@ def run_test(args):
         path = os.path.join(args.save_dir, "lstm", "QP_{}_{}_{}_{}_{}_results.mat".format(
             args.num_var, args.num_eq, args.num_ineq, args.outer_T, args.hidden_dim))
         os.makedirs(os.path.dirname(path), exist_ok=True)
-        sio.savemat(path, {"time": total_time, "x": last["x"].cpu().numpy(),
-                           "objs": np.array([r["obj"] for r in reports]),
-                           "ls_res": np.array([r["ls_res"] for r in reports]),
-                           "primal_res": np.array([r["primal"] for r in reports]),
-                           "dual_res": np.array([r["dual"] for r in reports])})
+        sio.savemat(path, results_dict(args, total_time, last["x"].cpu().numpy(), reports))
     return reports, total_time
+
+
+def timed_seconds(spans):
+    """Parallel Time of one batch: the solver's timed spans (scaling, iterations, unscale, Stage II
+    factor + iterations = the reference's timed model()/exact_model() calls, main.py:881-890,
+    1055-1066) without the per-kernel ("k:") and per-iteration metric ("hist:") spans."""
+    return sum(v for k, v in spans.items() if not k.startswith(("k:", "hist:"))) / 1e3
+
+
+COND_KEYS = ("x_cond_1_left", "x_cond_1_right", "x_cond_2_left", "x_cond_2_right", "z_cond_1_left",
+             "z_cond_1_right", "z_cond_2_left", "z_cond_2_right", "alpha_cond_left", "alpha_cond_right")
+
+
+def results_dict(args, total_time, x, reports):
+    """The --save_sol .mat content with the reference's key set and array shapes
+    (main.py:1226-1264):
+      objs / ls_res / primal_res / dual_res   [batches, T]  per-batch means per iteration;
+      *_fr (Stage II)  main.py:1099-1115 append each batch's list once per Stage-II iteration, so
+        objs_fr / primal_res_fr / dual_res_fr are [batches * F, F] (each batch's row F times),
+        while ls_res_fr is re-bound per batch (main.py:1052) and holds the last batch's [F];
+      *_cond_*  theoretical-condition lists whose computation is commented out in the reference
+        (main.py:903-944): one empty list per batch -> [batches, 0]."""
+    nb = len(reports)
+    d = {"time": total_time, "x": x,
+         "objs": np.array([r["obj"] for r in reports]),
+         "ls_res": np.array([r["ls_res"] for r in reports]),
+         "primal_res": np.array([r["primal"] for r in reports]),
+         "dual_res": np.array([r["dual"] for r in reports])}
+    if args.feas_rest:
+        F = args.feas_rest_num
+        rep = lambda k: np.array([r[k] for r in reports for _ in range(F)])  # noqa: E731
+        d.update(objs_fr=rep("fr_obj"), ls_res_fr=np.array(reports[-1]["fr_ls_res"]),
+                 primal_res_fr=rep("fr_primal"), dual_res_fr=rep("fr_dual"))
+    for k in COND_KEYS:
+        d[k] = np.zeros((nb, 0))
+    return d
 
 
 def _instances(args, ids, device):
@@ -235,6 +266,34 @@ def _instances(args, ids, device):
         d.update(G=d["A0"][:, :mi], A=d["A0"][:, mi:], c=d["zu"][:, :mi], b=d["zu"][:, mi:])
         return d
     return load_qp_instances(args, ids, device)
+
+
+def report_stats(d, x, mi, me, dist):
+    """Objective and constraint violations of an unscaled iterate x [B,n] (main.py:367-379,
+    497-516): obj mean, ineq/eq violation max-per-instance mean and elementwise mean.  With
+    ``dist`` the means are combined over ranks (each rank holds an equal share of the batch)."""
+    B = x.shape[0]
+    obj, _, _ = ops.metrics(d["Q"], d["p"].reshape(B, -1).contiguous(), d["A0"], x,
+                            torch.zeros(B, d["A0"].shape[1], device=x.device),
+                            torch.zeros(B, d["A0"].shape[1], device=x.device))
+    vals = [obj.mean()]
+    if mi:
+        iv = ops.bmv(d["G"].contiguous(), x, d["c"].reshape(B, -1).contiguous(), ops.BMV_POS_EXCESS)
+        vals += [iv.max(1).values.mean(), iv.mean()]
+    if me:
+        ev = ops.bmv(d["A"].contiguous(), x, d["b"].reshape(B, -1).contiguous(), ops.BMV_ABS_GAP)
+        vals += [ev.max(1).values.mean(), ev.mean()]
+    t = torch.stack(vals).double()
+    if dist is not None and dist.is_initialized() and dist.get_world_size() > 1:
+        dist.all_reduce(t)
+        t /= dist.get_world_size()
+    t = t.tolist()
+    out = {"obj": t.pop(0)}
+    if mi:
+        out["ineq_max"], out["ineq_mean"] = t.pop(0), t.pop(0)
+    if me:
+        out["eq_max"], out["eq_mean"] = t.pop(0), t.pop(0)
+    return out
 
 
 def run_train(args):
@@ -264,16 +323,27 @@ def run_train(args):
         model.train()
         t0 = time.time()
         loss = float("nan")
+        last = {}
         for bi in range(int(len(train_ids) / args.batch_size)):
             ids = train_ids[bi * args.batch_size:(bi + 1) * args.batch_size]
             first, count = parallel.shard(len(ids), world, rank)
             d = _instances(args, ids[first:first + count], device)
+            Dsc = None
             if args.scaling:
-                Qs, ps, As, zls, zus, _, _, _ = ops.ruiz_scale(d["Q"], d["p"], d["A0"], d["zl"], d["zu"], args.scaling_ites)
-                d = dict(Q=Qs, p=ps, A0=As, zl=zls, zu=zus)
-            loss = train.tbptt_batch(model, d, mi, me, args.outer_T, args.truncated_length, args.sigma, optimizer,
-                                     micro_batch=args.micro_batch or None, global_batch=len(ids), dist=dist)
+                Qs, ps, As, zls, zus, Dsc, _, _ = ops.ruiz_scale(d["Q"], d["p"], d["A0"], d["zl"], d["zu"],
+                                                                 args.scaling_ites)
+                ds = dict(Q=Qs, p=ps, A0=As, zl=zls, zu=zus)
+            else:
+                ds = d
+            fin = {}
+            loss = train.tbptt_batch(model, ds, mi, me, args.outer_T, args.truncated_length, args.sigma, optimizer,
+                                     micro_batch=args.micro_batch or None, global_batch=len(ids), dist=dist,
+                                     final=fin)
+            last = dict(d=d, x=fin["x"].reshape(count, -1) * (Dsc.reshape(count, -1) if Dsc is not None else 1.0))
         train_time = time.time() - t0
+        # main.py:362-379: objective and violations of the last training batch's final iterate
+        # (unscaled); each rank holds its shard, so the means are combined over ranks
+        tr = report_stats(last["d"], last["x"].contiguous(), mi, me, dist) if last else None
         # validation: full unroll under no_grad (main.py:382-510), metrics on unscaled x
         model.eval()
         t0 = time.time()
@@ -281,21 +351,21 @@ def run_train(args):
             v = _instances(args, val_ids, device)
             out = solver.solve(model, v["Q"], v["p"], v["A0"], v["zl"], v["zu"], mi, me, args.outer_T, args.sigma,
                                scaling=args.scaling, scaling_iters=args.scaling_ites, packed=packed)
-            x = out["x"].reshape(len(val_ids), -1).contiguous()
-            val_obj = float(out["obj"].mean())
-            vios = []
-            if mi:
-                vios.append(float(ops.bmv(v["G"].contiguous(), x, v["c"].reshape(len(val_ids), -1).contiguous(),
-                                          ops.BMV_POS_EXCESS).max(1).values.mean()))
-            if me:
-                vios.append(float(ops.bmv(v["A"].contiguous(), x, v["b"].reshape(len(val_ids), -1).contiguous(),
-                                          ops.BMV_ABS_GAP).max(1).values.mean()))
+            va = report_stats(v, out["x"].reshape(len(val_ids), -1).contiguous(), mi, me, None)
+            val_obj = va["obj"]
+            vios = ([va["ineq_max"]] if mi else []) + ([va["eq_max"]] if me else [])
         val_time = time.time() - t0
         stop = False
         if rank == 0:
             stop = stopper.step(val_obj, model, args.early_stop_mode or "min", args.eq_tol, *vios)
-            print("Epoch : {} | Train_Loss : {:.4f} | Val_Obj : {:.3f} | Train_Time : {:.3f} | Val_Time : {:.3f} |".format(
-                epoch, loss, val_obj, train_time, val_time), flush=True)
+            tobj = tr["obj"] if tr else float("nan")
+            print("Epoch : {} | Train_Obj : {:.3f} | Val_Obj : {:.3f} | Train_Time : {:.3f} | Val_Time : {:.3f} |".format(
+                epoch, tobj, val_obj, train_time, val_time), flush=True)
+            for key, name, on in (("ineq", "Ineq", mi), ("eq", "Eq", me)):
+                if on and tr:  # main.py:537-541
+                    print("Epoch : {} | Train_Max_{} : {:.3f} | Train_Mean_{} : {:.3f} | Val_Max_{} : {:.3f} | "
+                          "Val_Mean_{} : {:.3f} |".format(epoch, name, tr[key + "_max"], name, tr[key + "_mean"],
+                                                          name, va[key + "_max"], name, va[key + "_mean"]), flush=True)
         if dist is not None:
             flag = torch.tensor([1 if stop else 0], device=device)
             dist.broadcast(flag, 0)

@@ -23,9 +23,9 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _run(args, nproc=1, timeout=600):
+def _run(args, nproc=1, timeout=600, shared=True):
     env = dict(os.environ)
-    if nproc > 1:
+    if nproc > 1 and shared:
         env["IADMM_SHARED_GPU"] = "1"
         cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
                "--master-addr", "127.0.0.1", "--master-port", str(_free_port())] + args
@@ -55,7 +55,11 @@ def test_bench_single_gpu_contract():
     assert rf["bound"] == "mfma" and rf["unit"] == "TFLOP/s" and rf["launches"] == 2 * 3
     assert abs(rf["frac"] - rf["achieved"] / rf["peak"]) < 1e-9
     cb = r["cpu_baseline"]
-    assert cb["kind"] == "port" and cb["value"] > 0 and cb["cores"] >= 1
+    assert cb["kind"] == "port" and cb["value"] > 0 and cb["cores"] >= 1 and cb["cpu_model"]
+    # the GPU's result on the CPU sample's instances against the oracle's (same instances)
+    par = cb["parity"]["random-init"]
+    assert par["within_tol"], par
+    assert par["x_rel_l2"] <= par["tol"]["x"] and par["primal_max_rel"] <= par["tol"]["primal"]
     # the GPU and the CPU oracle solved the same instances: residuals of the same magnitude
     assert r["final_residual"]["primal_mean"] > 0
 
@@ -71,4 +75,27 @@ def test_bench_train_two_ranks_shared_gpu():
     r = _run(["bench_train.py", "--batch", "2", "--micro_batch", "1", "--steps", "1", "--warmup", "0",
               "--num_var", "32", "--num_ineq", "16", "--num_eq", "16", "--hidden_dim", "32", "--outer_T", "2"],
              nproc=2)
+    assert r["n_gpus"] == 2 and r["value"] > 0 and r["loss"] == r["loss"]
+
+
+def _need_two_gpus():
+    if torch.cuda.device_count() < 2:
+        pytest.skip("the RCCL path needs >= 2 GPUs (one rank per GPU)")
+
+
+def test_bench_two_ranks_rccl():
+    """Config 3's code path as it runs on a multi-GPU node: one rank per GPU, backend nccl (=
+    RCCL), no IADMM_SHARED_GPU.  Sharded instances, barrier, max-over-ranks timing."""
+    _need_two_gpus()
+    r = _run(["bench.py", "--batch", "4", "--steps", "1", "--warmup", "0", "--cpu-sample", "0"] + SMALL, nproc=2,
+             shared=False)
+    assert r["n_gpus"] == 2 and r["config"]["global_batch"] == 8 and r["value"] > 0
+
+
+def test_bench_train_two_ranks_rccl():
+    """Config 5's code path: the gradient all-reduce over RCCL, one rank per GPU."""
+    _need_two_gpus()
+    r = _run(["bench_train.py", "--batch", "2", "--micro_batch", "1", "--steps", "1", "--warmup", "0",
+              "--num_var", "32", "--num_ineq", "16", "--num_eq", "16", "--hidden_dim", "32", "--outer_T", "2"],
+             nproc=2, shared=False)
     assert r["n_gpus"] == 2 and r["value"] > 0 and r["loss"] == r["loss"]

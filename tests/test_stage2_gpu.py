@@ -54,8 +54,12 @@ def test_lu_pivots_match_lapack_choice(N):
     g = torch.Generator().manual_seed(7)
     K = torch.randn(2, N, N, generator=g)
     LU, piv, _ = ops.lu_factor(K.cuda().contiguous())
-    torch.set_num_threads(1)
-    lu_ref, ref = torch.linalg.lu_factor(K.double())
+    threads = torch.get_num_threads()
+    torch.set_num_threads(1)  # this torch build's multi-threaded MKL LASWP can hang
+    try:
+        lu_ref, ref = torch.linalg.lu_factor(K.double())
+    finally:
+        torch.set_num_threads(threads)
     assert torch.equal(piv.cpu().long(), ref.long() - 1)
     # same pivots -> the same factors up to fp32 rounding growth (L and U packed like LAPACK's)
     assert rel_l2(LU, lu_ref) < 1e-5

@@ -1,0 +1,90 @@
+"""Training gradients at the BASELINE config-5 instance shape (n=1000, m=500+500, h=800).
+
+The HIP forward + backward (models/lstm.py drop-in under autograd, utils.primal_dual_loss) of
+the reference's TBPTT loss (main.py:336-350) over T=2 iterations of B=2 Ruiz-scaled instances,
+against torch autograd through the oracle's restatement of the same iteration
+(oracle.lstm_iteration / oracle.primal_dual = models/lstm.py:47-96, utils.py:68-71) in fp32 AND
+in fp64.  The fp64 gradient separates the reference's own fp32 noise from slack in the kernels:
+the HIP gradient's distance to fp64 must be of the same order as the fp32 oracle's.
+
+Bounds: rel-L2 per parameter vs the fp32 oracle <= 2e-3 (the golden-fixture contract of
+test_train_gpu.py), and vs fp64 <= max(4 x the fp32 oracle's own error, 1e-5).
+"""
+import os
+
+import pytest
+import torch
+
+import iadmm_path  # noqa: F401
+from oracle import iadmm_oracle as orc
+
+pytestmark = pytest.mark.gpu
+
+N_VAR, MI, ME, H, T, B, SIGMA = 1000, 500, 500, 800, 2, 2, 6e-6
+
+
+def rel_l2(a, b):
+    a = torch.as_tensor(a).double().cpu()
+    b = torch.as_tensor(b).double().cpu()
+    return float((a - b).norm() / max(b.norm(), 1e-30))
+
+
+def oracle_grads(params, d, dtype):
+    prm = {k: v.detach().cpu().to(dtype).requires_grad_(True) for k, v in params.items()}
+    Q, p, A0, zl, zu = (d[k].cpu().to(dtype) for k in ("Q", "p", "A0", "zl", "zu"))
+    n, m = Q.shape[1], A0.shape[1]
+    x, y, z = (torch.zeros(B, r, 1, dtype=dtype) for r in (n, m, m))
+    xv = torch.zeros(B, n + m, 1, dtype=dtype)
+    Hs, Cs = torch.zeros(B, n + m, H, dtype=dtype), torch.zeros(B, n + m, H, dtype=dtype)
+    loss = 0.0
+    for t in range(T):
+        x, y, z, xv, Hs, Cs, _, _, _ = orc.lstm_iteration(prm, t, MI, ME, x, y, z, xv, SIGMA, Hs, Cs, Q, p, A0,
+                                                          zl, zu)
+        _, _, l = orc.primal_dual(x, y, z, Q, p, A0)
+        loss = loss + l.mean() / T
+    loss.backward()
+    return float(loss), {k: v.grad for k, v in prm.items()}
+
+
+def test_config5_shape_grads():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from iadmm import data, ops
+    from models.lstm import LSTM
+    import utils
+    raw = data.make_qp_batch(N_VAR, MI, ME, B, first_index=0, device="cuda")
+    Qs, ps, As, zls, zus, _, _, _ = ops.ruiz_scale(raw["Q"], raw["p"], raw["A0"], raw["zl"], raw["zu"], 10)
+    d = dict(Q=Qs, p=ps, A0=As, zl=zls, zu=zus)
+    torch.manual_seed(17)
+    model = LSTM(MI + ME, 2, H, T, "cuda")
+    model.train()
+    m = MI + ME
+    x, y, z = (torch.zeros(B, r, 1, device="cuda") for r in (N_VAR, m, m))
+    xv = torch.zeros(B, N_VAR + m, 1, device="cuda")
+    Hs, Cs = torch.zeros(B, N_VAR + m, H, device="cuda"), torch.zeros(B, N_VAR + m, H, device="cuda")
+    loss = 0.0
+    for t in range(T):
+        x, y, z, xv, Hs, Cs, _, _, _ = model(t, MI, ME, x, y, z, xv, SIGMA, Hs, Cs, lb=None, ub=None, **d)
+        _, _, l = utils.primal_dual_loss(x, y, z, d["Q"], d["p"], d["A0"])
+        loss = loss + l.mean() / T
+    loss.backward()
+    params = {k: v.detach() for k, v in model.named_parameters()}
+    threads = torch.get_num_threads()
+    torch.set_num_threads(max(1, min(16, os.cpu_count() or 1)))
+    try:
+        l32, g32 = oracle_grads(params, d, torch.float32)
+        l64, g64 = oracle_grads(params, d, torch.float64)
+    finally:
+        torch.set_num_threads(threads)
+    assert abs(float(loss) - l64) <= 1e-4 * abs(l64)
+    report, bad = {}, {}
+    for k, prm in model.named_parameters():
+        e32 = rel_l2(prm.grad, g32[k])
+        e64 = rel_l2(prm.grad, g64[k])
+        o64 = rel_l2(g32[k], g64[k])
+        report[k] = (e32, e64, o64)
+        if e32 > 2e-3 or e64 > max(4 * o64, 1e-5):
+            bad[k] = report[k]
+    print("[config5 grads] (vs fp32 oracle, vs fp64, fp32 oracle vs fp64):",
+          {k: tuple(f"{v:.1e}" for v in r) for k, r in report.items()})
+    assert not bad, bad
