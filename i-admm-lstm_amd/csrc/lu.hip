@@ -2,14 +2,14 @@
 // (reference: models/lu.py:26-35, torch.lu / torch.lu_solve on K[B,N,N]).
 //
 // Right-looking blocked LU in 64-column blocks (the ?getrf structure), each block factored as
-// four 16-column panels:
-//   lu_panel_kernel        one workgroup per instance: the (N-k) x 16 panel is factored in registers
+// four 16-column panels (N <= 2048) or eight 8-column panels (2048 < N <= 10240):
+//   lu_panel_kernel        one workgroup per instance: the (N-k) x 16 (x 8) panel is factored in registers
 //                          (pivot = first max |a| like LAPACK i?amax; the multipliers use a
 //                          reciprocal like ?getf2), the row interchanges are applied to the
 //                          block's other columns (?laswp), and U = L11^-1 A is solved for the
 //                          panel rows inside the current 64-column block.
 //   lu_update_block_kernel A -= L21 U12 on the columns of the current block right of the panel
-//                          (<= 48 columns, rows below the panel).
+//                          (<= 48 (56) columns, rows below the panel).
 // and, once per block, on the columns right of it:
 //   lu_swap_trsm_block_kernel the block's row interchanges on the columns outside it, and
 //                          U12 = L11^-1 A12 for its 64 rows (L11 in LDS; one thread per column).
@@ -34,7 +34,10 @@ namespace iadmm {
 typedef float floatx16 __attribute__((ext_vector_type(16)));
 
 constexpr int kNB = 16;
-constexpr int kPanelMaxM = 12;     // panel rows per thread: N <= 12 * 256
+constexpr int kPanelMaxM = 8;      // panel rows per thread: N <= 8 * 256 (12 rows spilled 782 VGPRs)
+constexpr int kBigNB = 8;          // panel width above N = 8 * 256
+constexpr int kBigThreads = 1024;  // panel workgroup size above N = 8 * 256
+constexpr int kBigMaxM = 10;       // rows per thread there: N <= 10 * 1024 (12 spills at 128 VGPRs)
 constexpr int kLuThreads = 256;
 constexpr int kUpdRows = 64;
 constexpr int kSolveBlk = 64;
@@ -81,20 +84,27 @@ IADMM_DEV void build_row_perm(const int* pv, int base, int n, int* rowid, int* c
 // index on ties), the owners of rows j and p exchange them through LDS, every thread scales its
 // rows below j by the reciprocal and applies the rank-1 update in registers.  M = ceil((N-k0)/256)
 // rounded up to the next instantiated size.
-IADMM_DEV float col_of(const float (&row)[kNB], int j) {  // row[j] for a run-time j, registers only
+template <int NB>
+IADMM_DEV float col_of(const float (&row)[NB], int j) {  // row[j] for a run-time j, registers only
   float v = row[0];
 #pragma unroll
-  for (int c = 1; c < kNB; ++c) v = c == j ? row[c] : v;
+  for (int c = 1; c < NB; ++c) v = c == j ? row[c] : v;
   return v;
 }
 
-template <int M>
-__global__ __launch_bounds__(kLuThreads, 2) void lu_panel_kernel(int N, int K0, int k0, int cend, float* A, int* piv,
-                                                                  int* info) {
+// Panel shapes: <M, 16, 256> (2 workgroups per CU) for N <= 8 * 256 = 2048; above that
+// <M, 8, 1024>: one 16-wave workgroup per CU holds up to 10 * 1024 = 10240 panel rows in
+// registers (an 8-wide panel keeps 10 rows per thread within the 128 VGPRs a 1024-thread
+// workgroup allows; 12 rows spill), so the pivot search still sees the whole column without
+// leaving registers.
+template <int M, int NB, int NT>
+__global__ __launch_bounds__(NT, NT <= 256 ? 2 : 1) void lu_panel_kernel(int N, int K0, int k0, int cend, float* A,
+                                                                         int* piv, int* info) {
+  constexpr int kNB = NB, kLuThreads = NT, NWV = NT / 64;
   __shared__ float xrow[2][kNB];            // [0] = row j, [1] = pivot row (after the exchange: row j)
   __shared__ float L11[kNB][kNB + 1];
-  __shared__ float rv[4];
-  __shared__ int ri[5];
+  __shared__ float rv[NWV];
+  __shared__ int ri[NWV + 1];
   __shared__ int pvs[kNB], prow[2 * kNB], pcur[2 * kNB], pcnt[1];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const size_t b = blockIdx.x;
@@ -150,16 +160,16 @@ __global__ __launch_bounds__(kLuThreads, 2) void lu_panel_kernel(int N, int K0, 
       if (tid == 0) {
         float bv = rv[0];
         int bx = ri[0];
-        for (int w = 1; w < kLuThreads / 64; ++w)
+        for (int w = 1; w < NWV; ++w)
           if (rv[w] > bv || (rv[w] == bv && ri[w] < bx)) { bv = rv[w]; bx = ri[w]; }
         if (bx >= R) bx = j;  // all entries NaN: keep the diagonal
         else if (bv == 0.f && info[b] == 0) info[b] = k0 + j + 1;
-        ri[4] = bx;
+        ri[NWV] = bx;
         piv[b * N + k0 + j] = k0 + bx;
         pvs[j] = k0 + bx;
       }
       __syncthreads();
-      const int p = ri[4];
+      const int p = ri[NWV];
       // the owner of row p publishes it and takes row j's values
 #pragma unroll
       for (int m = 0; m < M; ++m)
@@ -257,8 +267,10 @@ __global__ __launch_bounds__(kLuThreads, 2) void lu_panel_kernel(int N, int K0, 
 }
 
 // A[c0.., c0..cend) -= L21 U12 inside the current 64-column block, c0 = k0 + 16: rows
-// [c0 + blockIdx.y*64, +64) of instance blockIdx.x, w = cend - c0 <= 48 columns.
+// [c0 + blockIdx.y*64, +64) of instance blockIdx.x, w = cend - c0 <= 64 - NB columns.
+template <int NB>
 __global__ __launch_bounds__(256) void lu_update_block_kernel(int N, int k0, int cend, float* A) {
+  constexpr int kNB = NB;
   __shared__ float Us[kNB][kBlk - kNB];
   __shared__ float Ls[kUpdRows][kNB + 1];
   const int tid = threadIdx.x;
@@ -637,20 +649,37 @@ static int lu_factor_blocks(int64_t B, int64_t N, float* A, int* piv, int* info,
   IADMM_ALLOW_LDS(lu_trail_kernel<false>, kTrailLds);
   for (int K0 = 0; K0 < N; K0 += kBlk) {
     const int cend = (int)std::min<int64_t>(N, K0 + kBlk);
-    for (int k0 = K0; k0 < cend; k0 += kNB) {
-      const int R = (int)N - k0;
-      const dim3 g((unsigned)B), t(kLuThreads);
-      if (R <= kLuThreads) hipLaunchKernelGGL(lu_panel_kernel<1>, g, t, 0, s, (int)N, K0, k0, cend, A, piv, info);
-      else if (R <= 2 * kLuThreads) hipLaunchKernelGGL(lu_panel_kernel<2>, g, t, 0, s, (int)N, K0, k0, cend, A, piv, info);
-      else if (R <= 4 * kLuThreads) hipLaunchKernelGGL(lu_panel_kernel<4>, g, t, 0, s, (int)N, K0, k0, cend, A, piv, info);
-      else if (R <= 8 * kLuThreads) hipLaunchKernelGGL(lu_panel_kernel<8>, g, t, 0, s, (int)N, K0, k0, cend, A, piv, info);
-      else hipLaunchKernelGGL(lu_panel_kernel<kPanelMaxM>, g, t, 0, s, (int)N, K0, k0, cend, A, piv, info);
-      IADMM_CHECK_LAUNCH();
-      const int c0 = k0 + kNB;
-      if (c0 < cend) {
-        const dim3 grid((unsigned)B, (unsigned)((N - c0 + kUpdRows - 1) / kUpdRows));
-        hipLaunchKernelGGL(lu_update_block_kernel, grid, dim3(256), 0, s, (int)N, k0, cend, A);
+    if (N <= kPanelMaxM * kLuThreads) {
+      for (int k0 = K0; k0 < cend; k0 += kNB) {
+        const int R = (int)N - k0;
+        const dim3 g((unsigned)B), t(kLuThreads);
+        if (R <= kLuThreads) hipLaunchKernelGGL((lu_panel_kernel<1, kNB, kLuThreads>), g, t, 0, s, (int)N, K0, k0, cend, A, piv, info);
+        else if (R <= 2 * kLuThreads) hipLaunchKernelGGL((lu_panel_kernel<2, kNB, kLuThreads>), g, t, 0, s, (int)N, K0, k0, cend, A, piv, info);
+        else if (R <= 4 * kLuThreads) hipLaunchKernelGGL((lu_panel_kernel<4, kNB, kLuThreads>), g, t, 0, s, (int)N, K0, k0, cend, A, piv, info);
+        else hipLaunchKernelGGL((lu_panel_kernel<kPanelMaxM, kNB, kLuThreads>), g, t, 0, s, (int)N, K0, k0, cend, A, piv, info);
         IADMM_CHECK_LAUNCH();
+        const int c0 = k0 + kNB;
+        if (c0 < cend) {
+          const dim3 grid((unsigned)B, (unsigned)((N - c0 + kUpdRows - 1) / kUpdRows));
+          hipLaunchKernelGGL(lu_update_block_kernel<kNB>, grid, dim3(256), 0, s, (int)N, k0, cend, A);
+          IADMM_CHECK_LAUNCH();
+        }
+      }
+    } else {  // N > 2048: 8-wide panels on 1024-thread workgroups (N <= kBigMaxM * kBigThreads)
+      for (int k0 = K0; k0 < cend; k0 += kBigNB) {
+        const int R = (int)N - k0;
+        const dim3 g((unsigned)B), t(kBigThreads);
+        if (R <= 2 * kBigThreads) hipLaunchKernelGGL((lu_panel_kernel<2, kBigNB, kBigThreads>), g, t, 0, s, (int)N, K0, k0, cend, A, piv, info);
+        else if (R <= 4 * kBigThreads) hipLaunchKernelGGL((lu_panel_kernel<4, kBigNB, kBigThreads>), g, t, 0, s, (int)N, K0, k0, cend, A, piv, info);
+        else if (R <= 8 * kBigThreads) hipLaunchKernelGGL((lu_panel_kernel<8, kBigNB, kBigThreads>), g, t, 0, s, (int)N, K0, k0, cend, A, piv, info);
+        else hipLaunchKernelGGL((lu_panel_kernel<kBigMaxM, kBigNB, kBigThreads>), g, t, 0, s, (int)N, K0, k0, cend, A, piv, info);
+        IADMM_CHECK_LAUNCH();
+        const int c0 = k0 + kBigNB;
+        if (c0 < cend) {
+          const dim3 grid((unsigned)B, (unsigned)((N - c0 + kUpdRows - 1) / kUpdRows));
+          hipLaunchKernelGGL(lu_update_block_kernel<kBigNB>, grid, dim3(256), 0, s, (int)N, k0, cend, A);
+          IADMM_CHECK_LAUNCH();
+        }
       }
     }
     const int outside = K0 + ((int)N - cend);
@@ -675,7 +704,7 @@ static int lu_factor_blocks(int64_t B, int64_t N, float* A, int* piv, int* info,
 
 extern "C" int iadmm_lu_factor(int64_t B, int64_t N, float* A, int* piv, int* info, void* stream) {
   if (B <= 0 || N <= 0 || !A || !piv || !info) return IADMM_E_ARG;
-  if (N > kPanelMaxM * kLuThreads || B > 0x7fffffff) return IADMM_E_SIZE;
+  if (N > kBigMaxM * kBigThreads || B > 0x7fffffff) return IADMM_E_SIZE;
   hipStream_t s = (hipStream_t)stream;
   hipError_t e = hipMemsetAsync(info, 0, B * sizeof(int), s);
   if (e != hipSuccess) return (int)e;
@@ -693,7 +722,9 @@ extern "C" int iadmm_lu_solve(int64_t B, int64_t N, const float* LU, const int* 
                               void* stream) {
   if (B <= 0 || N <= 0 || !LU || !piv || !x) return IADMM_E_ARG;
   const size_t lds = ((size_t)N + kSolveBlk + kSolveBlk * kDS) * sizeof(float);
-  if (lds > 64 * 1024 || B > 0x7fffffff) return IADMM_E_SIZE;
+  if (lds > 160 * 1024 || B > 0x7fffffff) return IADMM_E_SIZE;  // gfx950: 160 KiB of LDS per workgroup
+  IADMM_ALLOW_LDS(lu_solve_kernel<true>, lds);
+  IADMM_ALLOW_LDS(lu_solve_kernel<false>, lds);
   if (N % 4 == 0 && aligned16(LU))
     hipLaunchKernelGGL(lu_solve_kernel<true>, dim3((unsigned)B), dim3(kSolveThreads), lds, (hipStream_t)stream,
                        (int)N, LU, piv, x);

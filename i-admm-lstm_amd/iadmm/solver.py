@@ -274,49 +274,78 @@ def fixed_alpha_scal(alpha, device):
     return s.to(device)
 
 
+def stage2_chunk(B, N, budget_bytes=None):
+    """Instances per Stage-II factorisation chunk: the dense K is 4 N^2 bytes per instance
+    (205 GB at config 4's N = 10000, B = 512), so the batch is factored in chunks that fit
+    ``budget_bytes`` (default: 80 % of the device's free memory).  Instances are independent, so
+    chunking changes nothing in the results."""
+    if budget_bytes is None:
+        free, _ = torch.cuda.mem_get_info()
+        budget_bytes = int(0.8 * free)
+    per = 4 * N * N + 64 * N  # K (factored in place) + pivots, rhs, solution, iterates
+    return max(1, min(B, budget_bytes // per))
+
+
 def stage2(Q, p, A0, zl, zu, rho_rows, x, y, z, sigma, iters, alpha=STAGE2_ALPHA, timer=None, iter_hook=None,
-           history=False):
+           history=False, chunk=None):
     """Stage II feasibility restoration (models/lu.py:13-47, driver main.py:1035-1066):
     factor K once (rho of the last Stage-I iteration), then ``iters`` exact ADMM steps with
     alpha-relaxation on x and z.  Works on the unscaled data like the reference.
     Q[B,n,n], p[B,n], A0[B,m,n], zl/zu/rho_rows[B,m], x[B,n], y/z[B,m].  Returns the iterates and
-    the factors (LU, piv).  A singular K raises (like models/lu.py's torch.lu check).
+    the factors (LU, piv) of the last chunk.  A singular K raises (like models/lu.py's torch.lu
+    check).  The batch is processed in chunks of ``chunk`` instances (default
+    :func:`stage2_chunk`: as many dense K as fit in memory).
     ``history=True`` records per-iteration obj / ls_res / primal / dual [4, iters, B] on the device
     (main.py:1068-1076: ls_res = ||K xv - b~|| with the solve's own K and b~) and
-    ``iter_hook(t, x, y, z)`` runs after every iteration; both in "hist:" timer spans."""
+    ``iter_hook(t, x, y, z, sl)`` runs after every iteration on the instances ``sl`` of the batch;
+    both in "hist:" timer spans."""
     timer = timer or Timer(False)
     B, n = x.shape
     m = y.shape[1]
+    N = n + m
     scal = fixed_alpha_scal(alpha, x.device)
-    tok = timer.start("stage2_factor")
-    K = ops.kkt_assemble(Q, A0, sigma, None, 0, rho_rows=rho_rows)
-    LU, piv, info = ops.lu_factor(K)
-    timer.stop(tok)
-    bad = int(info.max())  # one host read per factorisation
-    if bad:
-        raise RuntimeError(f"Stage II LU: U({bad},{bad}) is exactly zero (singular KKT matrix)")
     hist = torch.zeros(4, iters, B, dtype=torch.float32, device=x.device) if history else None
-    xv = None
-    for t in range(iters):
-        tok = timer.start("stage2_iterations")
-        b = ops.kkt_rhs(p, x, y, z, sigma, rho_rows=rho_rows)
-        xs = ops.lu_solve(LU, piv, b)
-        xv, x, y, z = ops.admm_update(n, m, 0, None, None, xs, x, y, z, zl, zu, scal, relax_z=True,
-                                      rho_rows=rho_rows)
+    step = int(chunk) if chunk else stage2_chunk(B, N)
+    xo, yo, zo = torch.empty_like(x), torch.empty_like(y), torch.empty_like(z)
+    xvo = torch.empty(B, N, dtype=x.dtype, device=x.device)
+    LU = piv = info = None
+    for s0 in range(0, B, step):
+        sl = slice(s0, min(B, s0 + step))
+        Qc, pc, Ac, zlc, zuc, rc = (t[sl] for t in (Q, p, A0, zl, zu, rho_rows))
+        xc, yc, zc = x[sl], y[sl], z[sl]
+        LU = piv = None  # the previous chunk's factors are released before the next K is built
+        tok = timer.start("stage2_factor")
+        K = ops.kkt_assemble(Qc, Ac, sigma, None, 0, rho_rows=rc)
+        LU, piv, info = ops.lu_factor(K)
         timer.stop(tok)
-        if history or iter_hook is not None:
-            htok = timer.start("hist:stage2")
-            if history:
-                r = ops.kkt_matvec(Q, A0, xv, sigma, None, 0, rho_rows=rho_rows) - b
-                hist[1, t].copy_(r.norm(dim=1))
-                o, pr, du = ops.metrics(Q, p, A0, x, y, z)
-                hist[0, t].copy_(o)
-                hist[2, t].copy_(pr)
-                hist[3, t].copy_(du)
-            if iter_hook is not None:
-                iter_hook(t, x, y, z)
-            timer.stop(htok)
-    out = dict(x=x, y=y, z=z, xv=xv, LU=LU, piv=piv, info=info)
+        bad = int(info.max())  # one host read per factorisation
+        if bad:
+            raise RuntimeError(f"Stage II LU: U({bad},{bad}) is exactly zero (singular KKT matrix)")
+        del K
+        xv = None
+        for t in range(iters):
+            tok = timer.start("stage2_iterations")
+            b = ops.kkt_rhs(pc, xc, yc, zc, sigma, rho_rows=rc)
+            xs = ops.lu_solve(LU, piv, b)
+            xv, xc, yc, zc = ops.admm_update(n, m, 0, None, None, xs, xc, yc, zc, zlc, zuc, scal, relax_z=True,
+                                             rho_rows=rc)
+            timer.stop(tok)
+            if history or iter_hook is not None:
+                htok = timer.start("hist:stage2")
+                if history:
+                    r = ops.kkt_matvec(Qc, Ac, xv, sigma, None, 0, rho_rows=rc) - b
+                    hist[1, t, sl] = r.norm(dim=1)
+                    o, pr, du = ops.metrics(Qc, pc, Ac, xc, yc, zc)
+                    hist[0, t, sl] = o
+                    hist[2, t, sl] = pr
+                    hist[3, t, sl] = du
+                if iter_hook is not None:
+                    iter_hook(t, xc, yc, zc, sl)
+                timer.stop(htok)
+        xo[sl], yo[sl], zo[sl] = xc, yc, zc
+        if xv is not None:
+            xvo[sl] = xv
+    out = dict(x=xo, y=yo, z=zo, xv=xvo if iters > 0 else None, LU=LU, piv=piv, info=info, chunk=step)
     if history:
         out.update(hist_obj=hist[0], hist_ls_res=hist[1], hist_primal=hist[2], hist_dual=hist[3])
     return out

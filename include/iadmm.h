@@ -100,13 +100,13 @@ int iadmm_kkt_rhs(int64_t B, int64_t n, int64_t m, int64_t num_ineq, const float
 
 /* Stage II batched LU with partial pivoting, in place (replaces torch.lu, models/lu.py:31):
  * A[B,N,N] -> packed L\U; piv[B,N] int32, 0-based (row i was swapped with piv[i]);
- * info[B] = first 1-based zero pivot or 0.  Right-looking in 64-column blocks (16-column panels, rank-64 MFMA
- * trailing update; limit N <= 3072).  Uses a B x 257-int stream-ordered scratch
+ * info[B] = first 1-based zero pivot or 0.  Right-looking in 64-column blocks (16-column panels up to N = 2048,
+ * 8-column panels on 1024-thread workgroups above; rank-64 MFMA trailing update; limit N <= 10240).  Uses a B x 257-int stream-ordered scratch
  * (hipMallocAsync / hipFreeAsync on `stream`). */
 int iadmm_lu_factor(int64_t B, int64_t N, float* A, int* piv, int* info, void* stream);
 
 /* Solve with the factors in place (replaces torch.lu_solve, models/lu.py:32,35): x[B,N] holds b
- * on entry and the solution on exit.  Limit N <= 12000. */
+ * on entry and the solution on exit.  Limit: (N + 4224) floats of LDS <= 160 KiB, N <= 36736. */
 int iadmm_lu_solve(int64_t B, int64_t N, const float* LU, const int* piv, float* x, void* stream);
 
 /* Pack the LSTM gate weights for the cell kernel (models/lstm.py:21-38 parameter layout).

@@ -172,13 +172,13 @@ def run_test(args):
                 F = args.feas_rest_num
                 fvio = torch.zeros(4, F, tb, device=device)
 
-                def fhook(t, x, y, z):
+                def fhook(t, x, y, z, sl):  # sl: the Stage-II chunk of the batch
                     if mi:
-                        iv = ops.bmv(G, x, c, ops.BMV_POS_EXCESS)
-                        fvio[0, t], fvio[1, t] = iv.max(1).values, iv.mean(1)
+                        iv = ops.bmv(G[sl].contiguous(), x, c[sl].contiguous(), ops.BMV_POS_EXCESS)
+                        fvio[0, t, sl], fvio[1, t, sl] = iv.max(1).values, iv.mean(1)
                     if me:
-                        ev = ops.bmv(A, x, b, ops.BMV_ABS_GAP)
-                        fvio[2, t], fvio[3, t] = ev.max(1).values, ev.mean(1)
+                        ev = ops.bmv(A[sl].contiguous(), x, b[sl].contiguous(), ops.BMV_ABS_GAP)
+                        fvio[2, t, sl], fvio[3, t, sl] = ev.max(1).values, ev.mean(1)
 
                 ftimer = solver.Timer(True)
                 rho_rows = solver.rho_rows_of(out["scal"], tb, mi + me, mi)

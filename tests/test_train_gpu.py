@@ -45,11 +45,13 @@ def test_grads_match_reference(golden):
         loss_tot = loss_tot + loss.mean() / T
     loss_tot.backward()
     assert abs(loss_tot.item() - float(g["train_loss"])) <= 1e-4 * abs(float(g["train_loss"]))
-    bad = {}
+    bad, worst = {}, 0.0
     for k, prm in model.named_parameters():
         err = rel_l2(prm.grad, g["grad_" + k])
+        worst = max(worst, err)
         if err > 2e-3:
             bad[k] = err
+    print(f"[grads {name}] max rel-L2 vs reference autograd {worst:.2e}")
     assert not bad, bad
 
 
