@@ -82,34 +82,36 @@ def main():
         info = int(out["info"].abs().sum())
         del out
     spans = {k: v / args.steps for k, v in timer.totals_ms().items()}
-    # per-kernel: time the factor's kernels and one solve separately with events
-    K = ops.kkt_assemble(d["Q"], d["A0"], 6e-6, None, 0, rho_rows=rho)
+    # per-kernel: time the factor's kernels and one solve separately with events, on the first
+    # chunk of instances whose dense K fits (all of them at config 2; config 4's 205 GB does not)
+    c = solver.stage2_chunk(B, N)
+    K = ops.kkt_assemble(d["Q"][:c], d["A0"][:c], 6e-6, None, 0, rho_rows=rho[:c].contiguous())
     e = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
     e[0].record()
     LU, piv, _ = ops.lu_factor(K)
     e[1].record()
-    b = ops.kkt_rhs(args_dev[1], x, y, z, 6e-6, rho_rows=rho)
+    b = ops.kkt_rhs(args_dev[1][:c], x[:c], y[:c], z[:c], 6e-6, rho_rows=rho[:c].contiguous())
     e[2].record()
     for _ in range(10):
         ops.lu_solve(LU, piv, b)
     e[3].record()
     torch.cuda.synchronize()
     fac_ms, solve_ms = e[0].elapsed_time(e[1]), e[2].elapsed_time(e[3]) / 10
-    upd_bytes = B * update_bytes(N)          # trailing updates, read + write
-    solve_bytes = B * (4.0 * N * N + 3 * 4.0 * N)  # L and U once, b in / x out
+    upd_bytes = c * update_bytes(N)          # trailing updates, read + write
+    solve_bytes = c * (4.0 * N * N + 3 * 4.0 * N)  # L and U once, b in / x out
     res = {
-        "metric": "Stage II (feasibility restoration) QP instances/s at n=1000 m=1000, "
+        "metric": f"Stage II (feasibility restoration) QP instances/s at n={n} m={m}, "
                   f"factor once + {args.iters} LU-solve iterations",
         "value": B * args.steps / el, "unit": "QP instances/s", "ms_per_step": 1e3 * el / args.steps,
         "n_gpus": 1, "dtype": "f32", "data": "synthetic (generate_data.py:67-76 distribution), random iterate",
         "config": {"workload": f"Stage II n={n} ineq={mi} eq={me} N={N} batch={B} feas_rest_num={args.iters}"},
         "phase_ms_per_step": spans, "singular_instances": info,
-        "factor": {"ms": fac_ms,
+        "factor": {"ms": fac_ms, "instances": c, "chunks_per_step": -(-B // c),
                    "trailing_update_GB": upd_bytes / 1e9,
                    "trailing_update_GBps_over_whole_factor": upd_bytes / fac_ms / 1e6,
                    "note": "a lower bound on the trailing-update kernel's own rate (the factor also runs panels, "
                            "interchanges and U12 solves); per-kernel times: profiles/r01_stage2_kernel_stats.csv",
-                   "tflops_equiv": B * (2.0 / 3.0) * N ** 3 / fac_ms / 1e9},
+                   "tflops_equiv": c * (2.0 / 3.0) * N ** 3 / fac_ms / 1e9},
         "roofline_solve": {"kernel": "iadmm_lu_solve", "bound": "hbm", "achieved": solve_bytes / solve_ms / 1e6,
                            "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": solve_bytes / solve_ms / 1e6 / HBM_PEAK_GBS,
                            "avg_launch_ms": solve_ms},
@@ -117,6 +119,7 @@ def main():
     if args.cpu_sample > 0:
         torch.set_num_threads(1)  # multi-threaded MKL getrf hangs on some KKT matrices
         c = min(args.cpu_sample, B)
+        del K, LU
         Kc = ops.kkt_assemble(d["Q"][:c], d["A0"][:c], 6e-6, None, 0, rho_rows=rho[:c].contiguous()).cpu()
         bc = b[:c].cpu().unsqueeze(-1)
         t0 = time.perf_counter()

@@ -279,9 +279,10 @@ def stage2_chunk(B, N, budget_bytes=None):
     (205 GB at config 4's N = 10000, B = 512), so the batch is factored in chunks that fit
     ``budget_bytes`` (default: 80 % of the device's free memory).  Instances are independent, so
     chunking changes nothing in the results."""
-    if budget_bytes is None:
+    if budget_bytes is None:  # free device memory + what torch's caching allocator holds unused
         free, _ = torch.cuda.mem_get_info()
-        budget_bytes = int(0.8 * free)
+        cached = torch.cuda.memory_reserved() - torch.cuda.memory_allocated()
+        budget_bytes = int(0.8 * (free + cached))
     per = 4 * N * N + 64 * N  # K (factored in place) + pivots, rhs, solution, iterates
     return max(1, min(B, budget_bytes // per))
 
