@@ -36,6 +36,7 @@ import torch  # noqa: E402
 
 FP32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md, Peak FP32 (matrix), spec
 HBM_PEAK_GBS = 8000.0           # MI355X_MICROARCH.md, HBM3E peak BW, spec
+KKT_KERNELS = ("kkt_split_p1", "kkt_split_c1", "kkt_split_p2", "kkt_split_c2")  # iadmm_kkt_resgrad
 
 
 def parse():
@@ -69,7 +70,8 @@ def parse():
 
 
 def pmc_traffic(kernel_prefix, n, m, h, B):
-    """Per-launch HBM-side bytes of one kernel from the committed rocprofv3 --pmc summaries of
+    """Per-launch HBM-side bytes of one operation (the sum over the kernels whose names contain one
+    of ``kernel_prefix``) from the committed rocprofv3 --pmc summaries of
     this exact workload (tools/pmc_summary.py output, one FETCH_SIZE and one WRITE_SIZE pass).
     gfx950 correction (MI355X_MICROARCH.md §HBM): FETCH_SIZE counts 128-B requests at 64 B, so
     it is doubled; WRITE_SIZE is taken as is.  Returns None when no matching profile exists."""
@@ -85,7 +87,8 @@ def pmc_traffic(kernel_prefix, n, m, h, B):
                 if any(k in r["kernel"] for k in names) and r["counter"] == ctr]
         if not rows:
             return None
-        tot += mult * float(rows[0]["mean"]) * 1024.0
+        # one launch of the operation = one dispatch of every kernel it consists of
+        tot += mult * sum(float(r["mean"]) for r in rows) * 1024.0
     return tot
 
 
@@ -329,7 +332,8 @@ def main():
                          "algorithmic_per_launch": cell_flop},
             "roofline_matvec": {"kernel": "iadmm_kkt_resgrad", "bound": "hbm", "achieved": kkt_gbs,
                                 "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": kkt_gbs / HBM_PEAK_GBS,
-                                "traffic": pmc_traffic("kkt_kernel<", n, mi + me, h, B),
+                                "traffic": pmc_traffic(KKT_KERNELS, n, mi + me, h, B),
+                                "kernels": "kkt_split_p1 + c1 + p2 + c2 (row-block split, csrc/kkt.hip)",
                                 "avg_launch_ms": ms_kkt, "launches": n_kkt,
                                 "algorithmic_per_launch": kkt_bytes},
             "phase_ms_per_step": {k: v / args.steps for k, v in spans.items() if not k.startswith("k:")},

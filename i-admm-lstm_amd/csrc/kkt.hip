@@ -122,6 +122,215 @@ __global__ __launch_bounds__(NT) void kkt_kernel(KktArgs a) {
   }
 }
 
+// ---- Row-block split of the residual gradient (any batch size fills the chip).
+// The rows of Q and of A0 are cut into fixed blocks of kRB rows (Q blocks 0..nbq-1, then A0
+// blocks nbq..nbq+nba-1); a workgroup streams a contiguous range of blocks, so an instance is
+// spread over S workgroups (S chosen from B: B*S ~ the chip's 1024 resident workgroup slots).  Row dots are complete
+// per row; column sums are formed per block (wave w owns rows w*U + 4U*k of the block; the
+// four waves are folded in order) and written as one partial vector per block, and the small
+// combine kernels add the partials in block order.  The summation order therefore depends on the
+// block structure only, never on S or B: every batch size and shard gives bitwise the same g.
+//   kkt_split_p1  dots = [Q x~ ; A0 x~], part[ia] = A0_ia^T v        (one read of Q and A0)
+//   kkt_split_c1  r = K xv - b~  (+ b~, rho_vec, r_out)
+//   kkt_split_p2  part[blk] = M_blk^T [r1 ; r2]_blk, dots_A0 = A0 r1 (one read of Q and A0)
+//   kkt_split_c2  g = [sum part + sigma r1 ; A0 r1 - r2 / rho]
+#ifndef IADMM_KKT_RB
+#define IADMM_KKT_RB 256
+#endif
+constexpr int kRB = IADMM_KKT_RB;  // rows per block (variant knob for tools/kktbench.py studies)
+
+struct KktSplitArgs {
+  int n, m, num_ineq, S, nbq, nba, dbuf;
+  const float *Q, *A0, *p, *x, *y, *z, *xv;
+  float sigma;
+  const float* scal;
+  float *dots, *part, *r;                // workspace: [B][N], [B][nbq+nba][n], [B][N]
+  float *g, *btild, *rhovec, *rout;
+};
+
+// One block of kRB rows starting at row0 of an [R x n] matrix Mx: wave w sweeps its rows over
+// all column panels (DOT: dot_s[r] for the block's rows, accumulated across panels), COL: the
+// block's column sums, folded over the 4 waves in order ((w0 + w1) + w2) + w3 into dst[n]
+// (global).  The fold is one round: every wave writes its partial panel into fold[wave][.] (LDS),
+// one barrier, then each thread sums its columns.  ``fold`` alternates between two buffers
+// (*fsel) when two fit, so the next fold's writes never meet this fold's reads without a
+// barrier in between; with one buffer a second barrier follows the reads.  c_s / dot_s are
+// indexed by the matrix's own row numbers.
+template <int NG, bool VEC, bool DOT, bool COL>
+IADMM_DEV void split_block(const float* __restrict__ Mx, int R, int n, int row0, const float* a_s,
+                           const float* c_s, float* dot_s, float* fold, int fstride, bool dbuf, int* fsel,
+                           float* __restrict__ dst, int wave, int lane) {
+  constexpr int PW = NG * 256;
+  const int rows = min(kRB, R - row0);
+  float col[NG * 4];
+#pragma unroll 1
+  for (int c0 = 0; c0 < n; c0 += PW) {
+    const int cp = n - c0 < PW ? n - c0 : PW;
+#pragma unroll
+    for (int i = 0; i < NG * 4; ++i) col[i] = 0.f;
+    // the waves interleave over the block's rows (wave w: rows w*U + 4U*k), so a workgroup reads
+    // one contiguous stretch of the matrix at a time (4 separate per-wave streams measured
+    // 5.3 TB/s per pass against 6.2 for the interleaved single-workgroup kernel)
+    sweep_panel<NG, VEC, DOT, COL>(Mx + (size_t)row0 * n + c0, rows, cp, n, a_s ? a_s + c0 : nullptr,
+                                   c_s ? c_s + row0 : nullptr, dot_s ? dot_s + row0 : nullptr, c0 > 0, col, wave, 4,
+                                   lane);
+    if constexpr (COL) {
+      float* f = fold + (dbuf ? *fsel : 0) * 4 * fstride;
+#pragma unroll
+      for (int idx = 0; idx < NG * 4; ++idx) {
+        const int c = col_of<NG, VEC>(lane, idx);
+        if (c < cp) f[wave * fstride + c] = col[idx];
+      }
+      __syncthreads();
+      for (int i = threadIdx.x; i < cp; i += blockDim.x) {
+        float v = f[i];
+        v += f[fstride + i];
+        v += f[2 * fstride + i];
+        v += f[3 * fstride + i];
+        dst[c0 + i] = v;
+      }
+      if (dbuf) *fsel ^= 1;
+      else __syncthreads();
+    }
+  }
+}
+
+// LDS of the split sweeps: two vectors (n + m floats) + the fold buffer(s) (4 x panel width each).
+__host__ __device__ inline int split_fstride(int n, int pw) { return n < pw ? n : pw; }
+
+// Variant knobs (tools/kktbench.py studies): minimum workgroups per CU the register allocation
+// must allow, and the LDS budget below which the fold is double-buffered.
+#ifndef IADMM_KKT_MINWG
+#define IADMM_KKT_MINWG 1
+#endif
+#ifndef IADMM_KKT_WG_TARGET
+#define IADMM_KKT_WG_TARGET 1024
+#endif
+#ifndef IADMM_KKT_DBUF_BYTES
+#define IADMM_KKT_DBUF_BYTES (64 * 1024)
+#endif
+
+template <int NG, bool VEC>
+__global__ __launch_bounds__(256, IADMM_KKT_MINWG) void kkt_split_p1(KktSplitArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  const int n = a.n, m = a.m, N = n + m, nblk = a.nbq + a.nba;
+  float* xs = sm;             // x~ [n]
+  float* vs = xs + n;         // v  [m]
+  float* fold = vs + m;       // [dbuf ? 2 : 1][4][fstride]
+  const int fstride = split_fstride(n, NG * 256);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const size_t b = blockIdx.x / a.S;
+  const int s = blockIdx.x % a.S;
+  const int lo = (int)((int64_t)s * nblk / a.S), hi = (int)((int64_t)(s + 1) * nblk / a.S);
+  const float* xvb = a.xv + b * N;
+  for (int i = tid; i < N; i += blockDim.x) {
+    if (i < n) xs[i] = xvb[i]; else vs[i - n] = xvb[i];
+  }
+  __syncthreads();
+  int fsel = 0;
+  float* db = a.dots + b * N;
+  for (int blk = lo; blk < hi; ++blk) {
+    if (blk < a.nbq) {
+      split_block<NG, VEC, true, false>(a.Q + b * n * n, n, n, blk * kRB, xs, nullptr, db, fold, fstride, a.dbuf,
+                                        &fsel, nullptr, wave, lane);
+    } else {
+      const int ia = blk - a.nbq;
+      split_block<NG, VEC, true, true>(a.A0 + b * m * n, m, n, ia * kRB, xs, vs, db + n, fold, fstride, a.dbuf,
+                                       &fsel, a.part + (b * nblk + ia) * n, wave, lane);
+    }
+  }
+}
+
+// Sum of the per-block partials k in [0, nb) of column i, in block order; the loads are issued
+// eight at a time (the adds stay sequential).
+IADMM_DEV float sum_partials(const float* __restrict__ pb, int nb, int n, int i) {
+  float red = 0.f;
+  int k = 0;
+  for (; k + 8 <= nb; k += 8) {
+    float v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = pb[(size_t)(k + u) * n + i];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) red += v[u];
+  }
+  for (; k < nb; ++k) red += pb[(size_t)k * n + i];
+  return red;
+}
+
+// Combine kernels: one thread per row of K (grid = B x ceil(N / 256)).
+__global__ __launch_bounds__(256) void kkt_split_c1(KktSplitArgs a, int nchunk) {
+  const int n = a.n, m = a.m, N = n + m, nblk = a.nbq + a.nba;
+  const size_t b = blockIdx.x / nchunk;
+  const int i = (blockIdx.x % nchunk) * 256 + threadIdx.x;
+  if (i >= N) return;
+  const float sigma = a.sigma;
+  const float* db = a.dots + b * N;
+  if (i < n) {
+    const float red = sum_partials(a.part + b * nblk * n, a.nba, n, i);
+    const float xi = a.xv[b * N + i];
+    const float b1 = sigma * a.x[b * n + i] - a.p[b * n + i];
+    const float r1 = ((db[i] + sigma * xi) + red) - b1;
+    a.r[b * N + i] = r1;
+    if (a.btild) a.btild[b * N + i] = b1;
+    if (a.rout) a.rout[b * N + i] = r1;
+  } else {
+    const int j = i - n;
+    const bool ineq = j < a.num_ineq;
+    const float rho = a.scal[ineq ? IADMM_S_RHO_IN : IADMM_S_RHO_EQ];
+    const float irho = a.scal[ineq ? IADMM_S_IRHO_IN : IADMM_S_IRHO_EQ];
+    const float b2 = a.z[b * m + j] - irho * a.y[b * m + j];
+    const float r2 = (db[i] + (-irho) * a.xv[b * N + i]) - b2;
+    a.r[b * N + i] = r2;
+    if (a.btild) a.btild[b * N + i] = b2;
+    if (a.rout) a.rout[b * N + i] = r2;
+    if (a.rhovec) a.rhovec[b * m + j] = rho;
+  }
+}
+
+template <int NG, bool VEC>
+__global__ __launch_bounds__(256, IADMM_KKT_MINWG) void kkt_split_p2(KktSplitArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  const int n = a.n, m = a.m, N = n + m, nblk = a.nbq + a.nba;
+  float* r1 = sm;
+  float* r2 = r1 + n;
+  float* fold = r2 + m;
+  const int fstride = split_fstride(n, NG * 256);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const size_t b = blockIdx.x / a.S;
+  const int s = blockIdx.x % a.S;
+  const int lo = (int)((int64_t)s * nblk / a.S), hi = (int)((int64_t)(s + 1) * nblk / a.S);
+  for (int i = tid; i < N; i += blockDim.x) {
+    if (i < n) r1[i] = a.r[b * N + i]; else r2[i - n] = a.r[b * N + i];
+  }
+  __syncthreads();
+  int fsel = 0;
+  float* db = a.dots + b * N;
+  for (int blk = lo; blk < hi; ++blk) {
+    float* dst = a.part + (b * nblk + blk) * n;
+    if (blk < a.nbq) {
+      split_block<NG, VEC, false, true>(a.Q + b * n * n, n, n, blk * kRB, nullptr, r1, nullptr, fold, fstride, a.dbuf,
+                                        &fsel, dst, wave, lane);
+    } else {
+      const int ia = blk - a.nbq;
+      split_block<NG, VEC, true, true>(a.A0 + b * m * n, m, n, ia * kRB, r1, r2, db + n, fold, fstride, a.dbuf,
+                                       &fsel, dst, wave, lane);
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void kkt_split_c2(KktSplitArgs a, int nchunk) {
+  const int n = a.n, m = a.m, N = n + m, nblk = a.nbq + a.nba;
+  const size_t b = blockIdx.x / nchunk;
+  const int i = (blockIdx.x % nchunk) * 256 + threadIdx.x;
+  if (i >= N) return;
+  if (i < n) {
+    a.g[b * N + i] = sum_partials(a.part + b * nblk * n, nblk, n, i) + a.sigma * a.r[b * N + i];
+  } else {
+    const float irho = a.scal[(i - n) < a.num_ineq ? IADMM_S_IRHO_IN : IADMM_S_IRHO_EQ];
+    a.g[b * N + i] = a.dots[b * N + i] + (-irho) * a.r[b * N + i];
+  }
+}
+
 struct MetricArgs {
   int n, m;
   const float *Q, *p, *A0, *x, *y, *z;
@@ -326,16 +535,72 @@ int launch_kkt(int64_t B, int64_t n, int64_t m, KktArgs a, hipStream_t s) {
 
 using namespace iadmm;
 
+template <int NG, bool VEC>
+static int launch_split(dim3 grid, size_t lds, const KktSplitArgs& a, hipStream_t s, int pass) {
+  if (pass == 1) {
+    IADMM_ALLOW_LDS((kkt_split_p1<NG, VEC>), lds);
+    hipLaunchKernelGGL((kkt_split_p1<NG, VEC>), grid, dim3(256), lds, s, a);
+  } else {
+    IADMM_ALLOW_LDS((kkt_split_p2<NG, VEC>), lds);
+    hipLaunchKernelGGL((kkt_split_p2<NG, VEC>), grid, dim3(256), lds, s, a);
+  }
+  IADMM_CHECK_LAUNCH();
+  return 0;
+}
+
+static int64_t kkt_split_blocks(int64_t n, int64_t m) { return (n + kRB - 1) / kRB + (m + kRB - 1) / kRB; }
+
+extern "C" int64_t iadmm_kkt_resgrad_ws_bytes(int64_t B, int64_t n, int64_t m) {
+  if (B <= 0 || n <= 0 || m < 0) return 0;
+  return B * (2 * (n + m) + kkt_split_blocks(n, m) * n) * (int64_t)sizeof(float);
+}
+
 extern "C" int iadmm_kkt_resgrad(int64_t B, int64_t n, int64_t m, int64_t num_ineq,
                                  const float* Q, const float* A0, const float* p, const float* x,
                                  const float* y, const float* z, const float* xv, float sigma,
                                  const float* scal, float* g, float* btild, float* rho_vec,
-                                 float* r_out, void* stream) {
+                                 float* r_out, void* ws, int64_t ws_bytes, void* stream) {
   if (B <= 0 || n <= 0 || m < 0 || num_ineq < 0 || num_ineq > m) return IADMM_E_ARG;
   if (!Q || !p || !x || !xv || !scal || !g || (m > 0 && (!A0 || !y || !z))) return IADMM_E_ARG;
-  if (!kkt_fits(n, m) || B > 0x7fffffff) return IADMM_E_SIZE;
-  KktArgs a{(int)n, (int)m, (int)num_ineq, Q, A0, p, x, y, z, xv, sigma, scal, g, btild, rho_vec, nullptr, r_out};
-  return launch_kkt<true>(B, n, m, a, (hipStream_t)stream);
+  if (!ws || ws_bytes < iadmm_kkt_resgrad_ws_bytes(B, n, m) || !aligned16(ws)) return IADMM_E_ARG;
+  const int64_t nbq = (n + kRB - 1) / kRB, nba = (m + kRB - 1) / kRB, nblk = nbq + nba;
+  const int ng = ng_for(n < kPanelNG * 256 ? n : kPanelNG * 256);
+  // LDS: the two vectors + one or two fold buffers (two while the total stays within 64 KiB, so
+  // that at least two workgroups share a CU; one otherwise)
+  const int64_t fstride = split_fstride((int)n, ng * 256);
+  const int64_t vec_floats = n + m;
+  const bool dbuf = (vec_floats + 8 * fstride) * 4 <= IADMM_KKT_DBUF_BYTES;
+  const size_t lds = (vec_floats + (dbuf ? 8 : 4) * fstride) * sizeof(float);
+  if (lds > 160 * 1024 || B > 0x7fffffff) return IADMM_E_SIZE;
+  // workgroups per instance: the batch's workgroups fill the chip's resident slots (4 per CU x
+  // 256 CUs) in ONE round -- a second, partial round of long streaming workgroups idles most of
+  // the chip at its end -- and at most one workgroup per block
+  int64_t S = IADMM_KKT_WG_TARGET / B;
+  S = S < 1 ? 1 : (S > nblk ? nblk : S);
+  if (B * S > 0x7fffffff || B * ((n + m + 255) / 256) > 0x7fffffff) return IADMM_E_SIZE;
+  float* w = static_cast<float*>(ws);
+  KktSplitArgs a{(int)n, (int)m, (int)num_ineq, (int)S, (int)nbq, (int)nba, dbuf ? 1 : 0, Q, A0, p, x, y, z, xv,
+                 sigma, scal, w, w + B * (n + m), w + B * (n + m) + B * nblk * n, g, btild, rho_vec, r_out};
+  const bool vec = (n % 4 == 0) && aligned16(Q) && (m == 0 || aligned16(A0));
+  hipStream_t s = (hipStream_t)stream;
+  const dim3 grid((unsigned)(B * S)), blk(256);
+  int rc = 0;
+  if (ng == 1) rc = vec ? launch_split<1, true>(grid, lds, a, s, 1) : launch_split<1, false>(grid, lds, a, s, 1);
+  else if (ng == 2) rc = vec ? launch_split<2, true>(grid, lds, a, s, 1) : launch_split<2, false>(grid, lds, a, s, 1);
+  else if (ng == 4) rc = vec ? launch_split<4, true>(grid, lds, a, s, 1) : launch_split<4, false>(grid, lds, a, s, 1);
+  else rc = vec ? launch_split<kPanelNG, true>(grid, lds, a, s, 1) : launch_split<kPanelNG, false>(grid, lds, a, s, 1);
+  if (rc) return rc;
+  const int nchunk = (int)((n + m + 255) / 256);
+  hipLaunchKernelGGL(kkt_split_c1, dim3((unsigned)(B * nchunk)), blk, 0, s, a, nchunk);
+  IADMM_CHECK_LAUNCH();
+  if (ng == 1) rc = vec ? launch_split<1, true>(grid, lds, a, s, 2) : launch_split<1, false>(grid, lds, a, s, 2);
+  else if (ng == 2) rc = vec ? launch_split<2, true>(grid, lds, a, s, 2) : launch_split<2, false>(grid, lds, a, s, 2);
+  else if (ng == 4) rc = vec ? launch_split<4, true>(grid, lds, a, s, 2) : launch_split<4, false>(grid, lds, a, s, 2);
+  else rc = vec ? launch_split<kPanelNG, true>(grid, lds, a, s, 2) : launch_split<kPanelNG, false>(grid, lds, a, s, 2);
+  if (rc) return rc;
+  hipLaunchKernelGGL(kkt_split_c2, dim3((unsigned)(B * nchunk)), blk, 0, s, a, nchunk);
+  IADMM_CHECK_LAUNCH();
+  return 0;
 }
 
 extern "C" int iadmm_kkt_lsres(int64_t B, int64_t n, int64_t m, int64_t num_ineq,

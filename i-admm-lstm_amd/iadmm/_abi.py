@@ -9,7 +9,8 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libiadmm.so")
+# IADMM_LIB_PATH: an alternative build of the same library (variant studies in tools/ only)
+LIB_PATH = os.environ.get("IADMM_LIB_PATH") or os.path.join(_HERE, "libiadmm.so")
 
 i64, f32, vp, cint = ctypes.c_int64, ctypes.c_float, ctypes.c_void_p, ctypes.c_int
 
@@ -18,7 +19,9 @@ SIGNATURES = {
     "iadmm_version": (cint, []),
     "iadmm_schedule": (cint, [vp, vp, i64, vp, vp]),
     "iadmm_schedule_fixed_alpha": (cint, [vp, f32, vp, vp]),
-    "iadmm_kkt_resgrad": (cint, [i64, i64, i64, i64, vp, vp, vp, vp, vp, vp, vp, f32, vp, vp, vp, vp, vp, vp]),
+    "iadmm_kkt_resgrad_ws_bytes": (i64, [i64, i64, i64]),
+    "iadmm_kkt_resgrad": (cint, [i64, i64, i64, i64, vp, vp, vp, vp, vp, vp, vp, f32, vp, vp, vp, vp, vp, vp, i64,
+                                 vp]),
     "iadmm_kkt_lsres": (cint, [i64, i64, i64, i64, vp, vp, vp, vp, vp, vp, vp, f32, vp, vp, vp]),
     "iadmm_lstm_packed_floats": (i64, [i64]),
     "iadmm_lstm_wx_floats": (i64, [i64]),

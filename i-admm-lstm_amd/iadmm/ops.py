@@ -54,14 +54,24 @@ def schedule_fixed_alpha(scal, alpha, out=None):
 
 
 # --------------------------------------------------------------------------- KKT
+def kkt_resgrad_ws(B, n, m, device):
+    """Workspace of iadmm_kkt_resgrad (row-dot, per-block partial and r vectors), reusable across
+    calls of the same (B, n, m)."""
+    nbytes = int(_abi.lib().iadmm_kkt_resgrad_ws_bytes(int(B), int(n), int(m)))
+    return torch.empty((nbytes + 3) // 4, dtype=torch.float32, device=device)
+
+
 def kkt_resgrad(Q, A0, p, x, y, z, xv, sigma, scal, num_ineq, g=None, btild=None, rho_vec=None,
-                r_out=None):
-    """g = K^T (K xv - b~) with the implicit KKT matrix (models/lstm.py:67-72)."""
+                r_out=None, ws=None):
+    """g = K^T (K xv - b~) with the implicit KKT matrix (models/lstm.py:67-72).  ``ws``: a
+    :func:`kkt_resgrad_ws` buffer (allocated per call when omitted)."""
     B, n = Q.shape[0], Q.shape[1]
     m = A0.shape[1]
     g = empty(B, n + m, like=Q) if g is None else g
+    ws = kkt_resgrad_ws(B, n, m, Q.device) if ws is None else ws
     _abi.call("iadmm_kkt_resgrad", B, n, m, int(num_ineq), _p(Q), _p(A0), _p(p), _p(x), _p(y), _p(z),
-              _p(xv), float(sigma), _p(scal), _p(g), _p(btild), _p(rho_vec), _p(r_out), _stream())
+              _p(xv), float(sigma), _p(scal), _p(g), _p(btild), _p(rho_vec), _p(r_out), _p(ws),
+              ws.numel() * 4, _stream())
     return g
 
 

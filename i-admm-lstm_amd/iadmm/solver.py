@@ -167,6 +167,7 @@ def solve(params, Q, p, A0, zl, zu, num_ineq, num_eq, T, sigma, scaling=True, sc
     C = torch.zeros(B, N, h, **f32)
     g = torch.empty(B, N, **f32)
     part = torch.empty(ops.lstm_ntiles(h), B * N, **f32)
+    kws = ops.kkt_resgrad_ws(B, n, m, dev)
     scal = torch.empty(ops.NSCAL, **f32)
     pv, zlv, zuv = ps.reshape(B, n), zls.reshape(B, m), zus.reshape(B, m)
     if history:
@@ -183,7 +184,7 @@ def solve(params, Q, p, A0, zl, zu, num_ineq, num_eq, T, sigma, scaling=True, sc
             tok = timer.start("iterations")
         ops.schedule(rho_p, alpha_p, t, out=scal)
         k = timer.start("k:kkt_resgrad")
-        ops.kkt_resgrad(Qs, As, pv, xs[cur], ys[cur], zs[cur], xvs[cur], sigma, scal, num_ineq, g=g)
+        ops.kkt_resgrad(Qs, As, pv, xs[cur], ys[cur], zs[cur], xvs[cur], sigma, scal, num_ineq, g=g, ws=kws)
         timer.stop(k)
         k = timer.start("k:lstm_cell")
         if f16:

@@ -66,12 +66,17 @@ int iadmm_schedule_fixed_alpha(const float* scal_in, float alpha, float* scal_ou
  * btild[B,n+m], rho_vec[B,m] and r_out[B,n+m] (= K xv - b~, kept for the training backward)
  * are optional outputs (may be NULL).
  * Rows [0,num_ineq) of A0 use rho_in, rows [num_ineq,m) rho_eq.
- * Limit: 3n + 2m <= 40960 (on-chip vectors). */
+ * The rows of Q and A0 are split into fixed 256-row blocks spread over enough workgroups to fill
+ * the chip at any B; column sums are combined per block in block order, so g does not depend on
+ * B (or on how a batch is sharded).  ws: caller-owned, 16-B aligned device workspace of at least
+ * iadmm_kkt_resgrad_ws_bytes(B, n, m) bytes.  Limit: 2n + m floats of LDS <= 160 KiB. */
+int64_t iadmm_kkt_resgrad_ws_bytes(int64_t B, int64_t n, int64_t m);
 int iadmm_kkt_resgrad(int64_t B, int64_t n, int64_t m, int64_t num_ineq,
                       const float* Q, const float* A0, const float* p,
                       const float* x, const float* y, const float* z, const float* xv,
                       float sigma, const float* scal,
-                      float* g, float* btild, float* rho_vec, float* r_out, void* stream);
+                      float* g, float* btild, float* rho_vec, float* r_out,
+                      void* ws, int64_t ws_bytes, void* stream);
 
 /* ||K xv - b~||_2 per instance (main.py:952 ``ls_res``), same implicit K. out[B]. */
 int iadmm_kkt_lsres(int64_t B, int64_t n, int64_t m, int64_t num_ineq,

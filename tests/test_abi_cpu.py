@@ -40,13 +40,20 @@ def test_size_queries_without_gpu():
     assert lib.iadmm_lstm_ntiles(40) == 2
     assert lib.iadmm_lstm_packed_floats(800) == 25 * 25 * 128 * 32
     assert lib.iadmm_version() > 0
+    # KKT workspace: dots + r (2 (n+m)) and one partial column-sum vector per 256-row block
+    assert lib.iadmm_kkt_resgrad_ws_bytes(3, 1000, 1000) == 3 * (2 * 2000 + (4 + 4) * 1000) * 4
+    assert lib.iadmm_kkt_resgrad_ws_bytes(1, 24, 0) == (2 * 24 + 1 * 24) * 4
 
 
 def test_bad_arguments_rejected_before_launch():
     # argument checks run on the host before any HIP call: safe without a GPU
     with pytest.raises(_abi.IadmmError, match="bad argument"):
-        _abi.call("iadmm_kkt_resgrad", 0, 10, 10, 5, *([None] * 7), 1.0, None, None, None, None, None, None)
+        _abi.call("iadmm_kkt_resgrad", 0, 10, 10, 5, *([None] * 7), 1.0, None, None, None, None, None, None, 0,
+                  None)
+    with pytest.raises(_abi.IadmmError, match="bad argument"):  # workspace missing / too small
+        _abi.call("iadmm_kkt_resgrad", 2, 10, 10, 5, *([16] * 7), 1.0, 16, 16, None, None, None, 16, 100, None)
     with pytest.raises(_abi.IadmmError, match="size beyond"):
-        _abi.call("iadmm_kkt_resgrad", 1, 20000, 20000, 0, *([1] * 7), 1.0, 1, 1, None, None, None, None)
+        _abi.call("iadmm_kkt_resgrad", 1, 20000, 20000, 0, *([16] * 7), 1.0, 16, 16, None, None, None, 16, 1 << 40,
+                  None)
     with pytest.raises(_abi.IadmmError, match="bad argument"):
         _abi.call("iadmm_lstm_cell_fwd", 10, 8, 16, 16, 16, 16, 16, 16, 16, 16, 16, None)

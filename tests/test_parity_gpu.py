@@ -224,3 +224,35 @@ def test_kkt_resgrad_panels(B, n, mi, me):
     assert rel_l2(g, ref) < 1e-5
     g2 = ops.kkt_resgrad(Q.to(DEV), A0.to(DEV), d(p), d(x), d(y), d(z), d(xv), sigma, scal, mi)
     assert torch.equal(g, g2)  # deterministic
+
+
+@pytest.mark.parametrize("n,mi,me", [(1000, 500, 500), (300, 130, 0), (77, 0, 50)])
+def test_kkt_resgrad_batch_invariant(n, mi, me):
+    """iadmm_kkt_resgrad splits each instance over B-dependent numbers of workgroups (1 or 128
+    instances: every 256-row block apart at n = m = 1000; 2048: whole instances),
+    but sums the per-block column partials in block order: g is bitwise the same whatever the batch
+    (and so whatever the shard), and matches the fp64 oracle at B = 1 and B = 128."""
+    from iadmm import ops
+    m = mi + me
+    B = 128
+    gen = torch.Generator().manual_seed(n + m)
+    r = lambda *s: torch.randn(*s, generator=gen)  # noqa: E731
+    Q, A0 = (r(B, n, n) / n ** 0.5).to(DEV), (r(B, m, n) / n ** 0.5).to(DEV)
+    p, x, y, z, xv = (r(B, k).to(DEV) for k in (n, n, m, m, n + m))
+    params = {"rho": torch.full((2, 1), 0.3, device=DEV), "alpha": torch.zeros(2, 1, device=DEV)}
+    scal = ops.schedule(params["rho"], params["alpha"], 0)
+    full = ops.kkt_resgrad(Q, A0, p, x, y, z, xv, 6e-6, scal, mi)
+    for i in (0, 77, B - 1):
+        one = ops.kkt_resgrad(*(t[i:i + 1].contiguous() for t in (Q, A0, p, x, y, z, xv)), 6e-6, scal, mi)
+        assert torch.equal(one[0], full[i]), i
+    big = 2048  # the same instances tiled: one workgroup per instance
+    rep = lambda t: t.repeat(big // B, *([1] * (t.dim() - 1))).contiguous()  # noqa: E731
+    if n * n + m * n <= 2_000_000:
+        tiled = ops.kkt_resgrad(*(rep(t) for t in (Q, A0, p, x, y, z, xv)), 6e-6, scal, mi)
+        assert torch.equal(tiled[:B], full) and torch.equal(tiled[-B:], full)
+    rv, _ = orc.schedule({k: v.cpu() for k, v in params.items()}, 0, y.cpu().unsqueeze(-1), mi, me)
+    K = orc.kkt_matrix(Q[:4].cpu().double(), A0[:4].cpu().double(), 6e-6, rv[:4].double())
+    bt = orc.kkt_rhs(x[:4].cpu().double().unsqueeze(-1), z[:4].cpu().double().unsqueeze(-1),
+                     y[:4].cpu().double().unsqueeze(-1), p[:4].cpu().double().unsqueeze(-1), 6e-6, rv[:4].double())
+    ref = orc.kkt_resgrad(K, bt, xv[:4].cpu().double().unsqueeze(-1)).reshape(4, -1)
+    assert rel_l2(full[:4], ref) < 1e-5

@@ -2,8 +2,9 @@
 through the HIP forward + backward kernels against the gradients the reference itself produced
 (tests/golden, autograd on the PyTorch-CPU reference).
 
-Tolerance: rel-L2 per parameter <= 2e-3 (summation-order noise of fp32 forward and backward
-accumulated over T unrolled iterations); the loss value <= 1e-4."""
+Tolerance: rel-L2 per parameter <= 1e-5 (measured r02: <= 6.5e-7 on every fixture, the divergent
+x10-weights one included; tests/test_train_config5_gpu.py shows at the config-5 shape that the HIP
+gradients sit as close to fp64 autograd as the fp32 reference itself); the loss value <= 1e-4."""
 import numpy as np
 import pytest
 import torch
@@ -11,6 +12,8 @@ import torch
 import iadmm_path  # noqa: F401
 
 pytestmark = pytest.mark.gpu
+
+GRAD_TOL = 1e-5
 
 
 def rel_l2(a, b):
@@ -49,7 +52,7 @@ def test_grads_match_reference(golden):
     for k, prm in model.named_parameters():
         err = rel_l2(prm.grad, g["grad_" + k])
         worst = max(worst, err)
-        if err > 2e-3:
+        if err > GRAD_TOL:
             bad[k] = err
     print(f"[grads {name}] max rel-L2 vs reference autograd {worst:.2e}")
     assert not bad, bad
