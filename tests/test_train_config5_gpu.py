@@ -7,8 +7,9 @@ against torch autograd through the oracle's restatement of the same iteration
 in fp64.  The fp64 gradient separates the reference's own fp32 noise from slack in the kernels:
 the HIP gradient's distance to fp64 must be of the same order as the fp32 oracle's.
 
-Bounds: rel-L2 per parameter vs the fp32 oracle <= 2e-3 (the golden-fixture contract of
-test_train_gpu.py), and vs fp64 <= max(4 x the fp32 oracle's own error, 1e-5).
+Bounds: rel-L2 per parameter vs the fp32 oracle <= 1e-5 (the golden-fixture contract of
+test_train_gpu.py; measured r02 <= 1.1e-6), and vs fp64 <= max(4 x the fp32 oracle's own error,
+1e-5) (measured: equal to the fp32 oracle's own distance, ~1.5e-5).
 """
 import os
 
@@ -83,7 +84,7 @@ def test_config5_shape_grads():
         e64 = rel_l2(prm.grad, g64[k])
         o64 = rel_l2(g32[k], g64[k])
         report[k] = (e32, e64, o64)
-        if e32 > 2e-3 or e64 > max(4 * o64, 1e-5):
+        if e32 > 1e-5 or e64 > max(4 * o64, 1e-5):
             bad[k] = report[k]
     print("[config5 grads] (vs fp32 oracle, vs fp64, fp32 oracle vs fp64):",
           {k: tuple(f"{v:.1e}" for v in r) for k, r in report.items()})
