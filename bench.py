@@ -61,6 +61,11 @@ def parse():
     ap.add_argument("--alt-f16x3", type=int, default=1,
                     help="also time one step of the optional split-precision cell (reported under "
                          "'alt_precision', never as the headline value)")
+    ap.add_argument("--lanes", type=int, default=0,
+                    help="instance lanes (HIP streams) of the solve; 0: solver.lanes_for(batch)")
+    ap.add_argument("--stage2-iters", type=int, default=20,
+                    help="feas_rest_num of a Stage II run (models/lu.py via main.py:1035-1066) on the solved "
+                         "batch, timed and reported under 'stage2' (0: skip)")
     ap.add_argument("--in-place-scaling", action="store_true",
                     help="scale Q/A0 in place (no unscaled copy; residuals via the scaling identity)")
     a = ap.parse_args()
@@ -69,17 +74,19 @@ def parse():
     return a
 
 
-def pmc_traffic(kernel_prefix, n, m, h, B):
-    """Per-launch HBM-side bytes of one operation (the sum over the kernels whose names contain one
-    of ``kernel_prefix``) from the committed rocprofv3 --pmc summaries of
-    this exact workload (tools/pmc_summary.py output, one FETCH_SIZE and one WRITE_SIZE pass).
+def pmc_traffic(kernel_prefix, n, m, h, B, lanes=1):
+    """HBM-side bytes of one operation per iteration of the whole batch (the sum over the kernels
+    whose names contain one of ``kernel_prefix``, times the lanes: one dispatch per lane) from the
+    committed rocprofv3 --pmc summaries of this exact workload (tools/pmc_summary.py output, one
+    FETCH_SIZE and one WRITE_SIZE pass; file suffix ``_L{lanes}`` when lanes > 1).
     gfx950 correction (MI355X_MICROARCH.md §HBM): FETCH_SIZE counts 128-B requests at 64 B, so
     it is doubled; WRITE_SIZE is taken as is.  Returns None when no matching profile exists."""
     import csv
     import glob
     tot = 0.0
     for ctr, mult in (("FETCH_SIZE", 2.0), ("WRITE_SIZE", 1.0)):
-        files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_pmc_{ctr}_n{n}_m{m}_h{h}_B{B}.csv")))
+        sfx = f"_L{lanes}" if lanes > 1 else ""
+        files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_pmc_{ctr}_n{n}_m{m}_h{h}_B{B}{sfx}.csv")))
         if not files:
             return None
         names = (kernel_prefix,) if isinstance(kernel_prefix, str) else kernel_prefix
@@ -88,7 +95,7 @@ def pmc_traffic(kernel_prefix, n, m, h, B):
         if not rows:
             return None
         # one launch of the operation = one dispatch of every kernel it consists of
-        tot += mult * sum(float(r["mean"]) for r in rows) * 1024.0
+        tot += mult * sum(float(r["mean"]) for r in rows) * 1024.0 * lanes
     return tot
 
 
@@ -171,6 +178,36 @@ def cpu_baseline(args, d, params, gpu_out, weights_tag, extra=()):
     return rec
 
 
+def stage2_record(args, d, out, n, mi, me, B):
+    """Time Stage II (solver.stage2: dense K, batched blocked LU, feas_rest_num solves) on the
+    solved batch; per-phase hipEvent times and instances/s."""
+    from iadmm import solver
+    m = mi + me
+    rho_rows = solver.rho_rows_of(out["scal"], B, m, mi)
+    x, y, z = (out[k].reshape(B, -1) for k in ("x", "y", "z"))
+    st_args = (d["Q"], d["p"].reshape(B, n), d["A0"], d["zl"].reshape(B, m), d["zu"].reshape(B, m), rho_rows,
+               x, y, z, args.sigma, args.stage2_iters)
+    r = solver.stage2(*st_args)
+    del r
+    tm = solver.Timer(True)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    r = solver.stage2(*st_args, timer=tm)
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    spans = tm.totals_ms()
+    from iadmm import ops
+    pr = ops.metrics(d["Q"], d["p"].reshape(B, n), d["A0"], r["x"], r["y"], r["z"])
+    rec = {"value": B / el, "unit": "QP instances/s", "feas_rest_num": args.stage2_iters, "ms": 1e3 * el,
+           "factor_ms": spans.get("stage2_factor"), "solve_iter_ms": spans.get("stage2_iterations", 0.0) / args.stage2_iters,
+           "chunk": r["chunk"], "final_primal_mean": float(pr[1].mean()), "final_dual_mean": float(pr[2].mean()),
+           "note": "Stage II (--feas_rest) on the solved batch: K assembled from the last Stage-I rho on the "
+                   "unscaled data, batched blocked LU (csrc/lu.hip) once, feas_rest_num solves + alpha=1.6 "
+                   "updates; outside the headline's timed scope"}
+    del r
+    return rec
+
+
 def load_weights(args, h, T):
     """(params dict on cuda, tag): the checkpoint named like main.py's (QP_{n}_{eq}_{ineq}_{T}_{h})
     under checkpoints/ for --weights auto, a given .pth, or random init."""
@@ -230,6 +267,8 @@ def main():
     elif not keep:
         master = None
 
+    lanes = args.lanes or solver.lanes_for(count)
+
     def step(timer, precision="f32", prm=None):
         if not keep and master is not None:
             for k in d:
@@ -237,7 +276,8 @@ def main():
             torch.cuda.synchronize()
         with torch.no_grad():
             return solver.solve(prm or params, d["Q"], d["p"], d["A0"], d["zl"], d["zu"], mi, me, T, args.sigma,
-                                keep_unscaled=keep, packed=None if prm else packed, timer=timer, precision=precision)
+                                keep_unscaled=keep, packed=None if prm else packed, timer=timer, precision=precision,
+                                lanes=lanes)
 
     for _ in range(args.warmup):
         step(None)
@@ -251,6 +291,7 @@ def main():
         if dist:
             dist.barrier()
         torch.cuda.synchronize()
+        out = None  # the previous step's state (H, C: 13 GB) is released before the next one allocates
         t0 = time.perf_counter()
         out = step(timer)
         torch.cuda.synchronize()
@@ -259,14 +300,26 @@ def main():
     elapsed = parallel.max_over_ranks(elapsed, dist, device="cuda")
     primal, dual = float(out["primal"].mean()), float(out["dual"].mean())
 
-    # dominant kernel and residual matvec, from the per-launch hipEvents of the timed steps
+    # dominant kernel and residual matvec, from the per-launch hipEvents of the timed steps.  With
+    # several lanes the launches of one kernel overlap (each covers B / lanes instances), so the
+    # achieved rate is the kernel's total algorithmic work over its busy time (the union of its
+    # launch intervals); with one lane that is work per launch / mean launch time.
     n_cell, ms_cell = timer.stats_ms("k:lstm_cell")
     n_kkt, ms_kkt = timer.stats_ms("k:kkt_resgrad")
+    busy_cell, busy_kkt = timer.busy_ms("k:lstm_cell"), timer.busy_ms("k:kkt_resgrad")
     spans = timer.totals_ms()
-    cell_flop = B * (8.0 * N * h * h + 18.0 * N * h)            # per launch
+    cell_flop = B * (8.0 * N * h * h + 18.0 * N * h)            # per instance-batch iteration
     kkt_bytes = B * (2.0 * (n * n + (mi + me) * n) * 4 + 10.0 * N * 4)
-    cell_tf = cell_flop / (ms_cell * 1e-3) / 1e12
-    kkt_gbs = kkt_bytes / (ms_kkt * 1e-3) / 1e9
+    iters = args.steps * T
+    cell_tf = cell_flop * iters / (busy_cell * 1e-3) / 1e12
+    kkt_gbs = kkt_bytes * iters / (busy_kkt * 1e-3) / 1e9
+
+    # Stage II (--feas_rest) on the solved batch, like main.py:1035-1066: K from the last Stage-I
+    # rho on the unscaled data, factored once, then feas_rest_num exact iterations (one warm-up run,
+    # one timed run; not part of the headline value, whose timed scope is the README test command)
+    st2 = None
+    if args.stage2_iters > 0 and keep:
+        st2 = stage2_record(args, d, out, n, mi, me, B)
 
     # optional split-precision mode: one step after the headline steps, reported beside it
     alt = None
@@ -283,11 +336,12 @@ def main():
         torch.cuda.synchronize()
         el16 = parallel.max_over_ranks(time.perf_counter() - t0, dist, device="cuda")
         n16, ms16 = timer16.stats_ms("k:lstm_cell")
+        busy16 = timer16.busy_ms("k:lstm_cell")
         alt = {"mode": "f16x3",
                "note": "optional split-precision gate GEMM (3-term fp16 split, fp32 accumulation, "
                        "csrc/lstm_f16x3.hip); not the headline value",
                "value": world * B / el16, "unit": "QP instances/s", "ms_per_step": 1e3 * el16,
-               "cell_avg_launch_ms": ms16, "cell_tflops_f32_equiv": cell_flop / (ms16 * 1e-3) / 1e12,
+               "cell_avg_launch_ms": ms16, "cell_tflops_f32_equiv": cell_flop * T / (busy16 * 1e-3) / 1e12,
                "final_residual": {"primal_mean": float(out16["primal"].mean()),
                                   "dual_mean": float(out16["dual"].mean())},
                "x_rel_l2_vs_f32_run": float((out16["x"] - x32).norm() / x32.norm().clamp_min(1e-30))}
@@ -318,26 +372,30 @@ def main():
             "dtype": "f32",
             "data": f"synthetic (generate_data.py:67-76 distribution, per-instance seeds); weights {weights_tag}",
             "config": {"workload": f"QP n={n} ineq={mi} eq={me} K={T} hidden={h} --test --scaling, "
-                                   f"batch={B}/GPU ({baseline_config(args, world)})",
+                                   f"batch={B}/GPU ({baseline_config(args, world)}), {lanes} lane(s)",
                        "global_batch": world * B, "num_var": n, "num_ineq": mi, "num_eq": me,
-                       "outer_T": T, "hidden_dim": h, "parallelism": f"instance-shard x{world}",
+                       "outer_T": T, "hidden_dim": h, "parallelism": f"instance-shard x{world}", "lanes": lanes,
                        "in_place_scaling": not keep},
             "final_residual": {"primal_mean": primal, "dual_mean": dual, "sum": primal + dual,
                                "weights": weights_tag},
             "roofline": {"kernel": "iadmm_lstm_cell_fwd", "bound": "mfma", "achieved": cell_tf,
                          "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": cell_tf / FP32_MFMA_PEAK_TFLOPS,
-                         "traffic": pmc_traffic(("cell_fwd_dma_kernel",), n, mi + me, h, B),
+                         "traffic": pmc_traffic(("cell_fwd_dma_kernel",), n, mi + me, h, B, lanes),
                          "traffic_source": "profiles/r*_pmc_{FETCH,WRITE}_SIZE_*.csv (separate --pmc passes)",
-                         "avg_launch_ms": ms_cell, "launches": n_cell,
-                         "algorithmic_per_launch": cell_flop},
+                         "avg_launch_ms": ms_cell, "launches": n_cell, "busy_ms_per_iteration": busy_cell / iters,
+                         "algorithmic_per_iteration": cell_flop,
+                         "algorithmic_per_launch": cell_flop / lanes},
             "roofline_matvec": {"kernel": "iadmm_kkt_resgrad", "bound": "hbm", "achieved": kkt_gbs,
                                 "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": kkt_gbs / HBM_PEAK_GBS,
-                                "traffic": pmc_traffic(KKT_KERNELS, n, mi + me, h, B),
+                                "traffic": pmc_traffic(KKT_KERNELS, n, mi + me, h, B, lanes),
                                 "kernels": "kkt_split_p1 + c1 + p2 + c2 (row-block split, csrc/kkt.hip)",
-                                "avg_launch_ms": ms_kkt, "launches": n_kkt,
-                                "algorithmic_per_launch": kkt_bytes},
+                                "avg_launch_ms": ms_kkt, "launches": n_kkt, "busy_ms_per_iteration": busy_kkt / iters,
+                                "algorithmic_per_iteration": kkt_bytes,
+                                "algorithmic_per_launch": kkt_bytes / lanes},
             "phase_ms_per_step": {k: v / args.steps for k, v in spans.items() if not k.startswith("k:")},
         }
+        if st2 is not None:
+            res["stage2"] = st2
         if alt is not None:
             res["alt_precision"] = alt
         if rand is not None:

@@ -18,6 +18,7 @@ struct CellArgsT {
   int h, njt, nkc32;
   const float *H, *C, *xv, *g, *Upk, *Wx;
   float *Hn, *Cn, *part;
+  int pgroup;  // panels per tile group of cell_tile_of_block_grouped (0 or 1: hidden tile fastest)
 };
 
 // XCD-aware bijective remap: blocks b, b+8, ... share an XCD; give each XCD a contiguous run of
@@ -28,6 +29,27 @@ IADMM_DEV void cell_tile_of_block(int njt, int& jt, int& rt) {
   const int logical = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + local;
   jt = logical % njt;
   rt = logical / njt;
+}
+
+// Grouped variant: the logical tiles (same XCD-contiguous ranges as above) are walked in groups of
+// pg row panels x all njt hidden tiles, hidden tile SLOWEST inside a group: the pg workgroups of
+// one hidden tile are dispatched back to back, so they stream the same weight slice at the same K
+// position (one L2 fill serves pg workgroups), while a panel's njt workgroups stay within one
+// group (pg * njt consecutive dispatches).  pg <= 1 is cell_tile_of_block.
+IADMM_DEV void cell_tile_of_block_grouped(int njt, int64_t nrt, int pg, int& jt, int& rt) {
+  if (pg <= 1) {
+    cell_tile_of_block(njt, jt, rt);
+    return;
+  }
+  const int nwg = gridDim.x, bid = blockIdx.x;
+  const int xcd = bid & 7, local = bid >> 3, q8 = nwg >> 3, r8 = nwg & 7;
+  const int logical = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + local;
+  const int S = pg * njt;
+  const int st = logical / S, r = logical - st * S;
+  const int p0 = st * pg;
+  const int pl = (int)(nrt - p0 < pg ? nrt - p0 : pg);
+  jt = r / pl;
+  rt = p0 + (r - jt * pl);
 }
 
 // acc[g][r] (4 gates x 2 row blocks of 32x32) = U_g[:, jt*32 .. +32]^T . H[rbase + wave*64 + r*32 ..]^T
@@ -490,7 +512,7 @@ __global__ __launch_bounds__(256, 2) void cell_fwd_dma_kernel(CellArgsT a) {
   float* ring = dsm;
   float* sW = dsm + kRingFloats;
   int jt, rt;
-  cell_tile_of_block(a.njt, jt, rt);
+  cell_tile_of_block_grouped(a.njt, (a.M + kRows - 1) / kRows, a.pgroup, jt, rt);
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int jl = lane & 31, hf = lane >> 5;

@@ -70,17 +70,22 @@ class PackedWeights:
 
 
 class Timer:
-    """hipEvent brackets on the current stream (named spans, summed)."""
+    """hipEvent brackets on the current stream (named spans, summed).  Spans of one name may run
+    on several streams at once (solve(lanes > 1)); :meth:`busy_ms` gives the time during which
+    at least one of them was running."""
 
     def __init__(self, enabled):
         self.enabled = enabled
         self.spans = {}
+        self.ref = None  # first event recorded: the time origin of busy_ms
 
     def start(self, name):
         if not self.enabled:
             return None
         ev = torch.cuda.Event(enable_timing=True)
         ev.record()
+        if self.ref is None:
+            self.ref = ev
         return (name, ev)
 
     def stop(self, tok):
@@ -102,16 +107,47 @@ class Timer:
             return 0, float("nan")
         return len(v), sum(a.elapsed_time(b) for a, b in v) / len(v)
 
+    def busy_ms(self, name):
+        """Length of the union of the intervals of span ``name`` (ms): equal to the summed
+        durations when the spans never overlap (one stream)."""
+        torch.cuda.synchronize()
+        iv = sorted((self.ref.elapsed_time(a), self.ref.elapsed_time(b)) for a, b in self.spans.get(name, []))
+        tot, end = 0.0, float("-inf")
+        for a, b in iv:
+            if a > end:
+                tot += b - a
+                end = b
+            elif b > end:
+                tot += b - end
+                end = b
+        return tot
+
     def reset(self):
         self.spans = {}
+        self.ref = None
 
 
 PRECISIONS = ("f32", "f16x3")
 
 
+def lanes_for(B):
+    """Default number of instance lanes of :func:`solve`: one.  Two staggered lanes measured +1.0 %
+    at the bench shape (130.7 against 129.4 instances/s on one box): the residual-matvec
+    workgroups (40 KiB of LDS) displace one of the cell kernel's two workgroups on a CU while they
+    run, so only part of the matvec hides behind the other lane's cell kernel."""
+    return 1
+
+
 def solve(params, Q, p, A0, zl, zu, num_ineq, num_eq, T, sigma, scaling=True, scaling_iters=10,
-          keep_unscaled=True, history=False, packed=None, timer=None, iter_hook=None, precision="f32"):
+          keep_unscaled=True, history=False, packed=None, timer=None, iter_hook=None, precision="f32",
+          lanes=None):
     """Solve one batch; returns a dict with unscaled x/y/z, scaled state, final residuals.
+
+    ``lanes``: the batch is cut into this many contiguous instance groups, each iterated on its own
+    HIP stream (default :func:`lanes_for`; 1 with ``history``).  Instances are independent and
+    every kernel is batch-invariant, so the result is bitwise the same for any lane count; the
+    point is overlap: while one lane runs the MFMA-bound cell kernel, another's HBM-bound residual
+    matvec and update kernels run beside it instead of in the cell kernels' gaps.
 
     Q[B,n,n], p[B,n,1], A0[B,m,n], zl/zu[B,m,1] fp32 device tensors (unscaled, Q already *2 as
     main.py:718 loads it).  ``keep_unscaled=False`` scales the data in place (saves 8 GB at the
@@ -154,25 +190,70 @@ def solve(params, Q, p, A0, zl, zu, num_ineq, num_eq, T, sigma, scaling=True, sc
     timer.stop(tok)
 
     # state (two sets) and work buffers
+    tok = timer.start("setup")
     xs = [torch.zeros(B, n, **f32), torch.empty(B, n, **f32)]
     ys = [torch.zeros(B, m, **f32), torch.empty(B, m, **f32)]
     zs = [torch.zeros(B, m, **f32), torch.empty(B, m, **f32)]
     xvs = [torch.zeros(B, N, **f32), torch.empty(B, N, **f32)]
-    if f16:  # split planes of H (ping-pong) + the fp32 H written on the last iteration
-        f16t = dict(dtype=torch.float16, device=dev)
-        H16s = [torch.zeros(2, B, N, h, **f16t), torch.empty(2, B, N, h, **f16t)]
+    if f16:  # the fp32 H is written on the last iteration only (split planes per lane below)
         Hs = [torch.zeros(B, N, h, **f32)] * 2
     else:
         Hs = [torch.zeros(B, N, h, **f32), torch.empty(B, N, h, **f32)]
     C = torch.zeros(B, N, h, **f32)
     g = torch.empty(B, N, **f32)
-    part = torch.empty(ops.lstm_ntiles(h), B * N, **f32)
-    kws = ops.kkt_resgrad_ws(B, n, m, dev)
-    scal = torch.empty(ops.NSCAL, **f32)
     pv, zlv, zuv = ps.reshape(B, n), zls.reshape(B, m), zus.reshape(B, m)
     if history:
         hist = torch.zeros(4, T, B, **f32)  # obj, ls_res, primal, dual
         tmp = (torch.empty(B, n, **f32), torch.empty(B, m, **f32), torch.empty(B, m, **f32))
+        lanes = 1
+    L = max(1, min(int(lanes if lanes is not None else lanes_for(B)), B))
+
+    main = torch.cuda.current_stream(dev)
+    lane = []  # per lane: instance slice, stream, its own scalars / projection partials / KKT workspace
+    for i in range(L):
+        b0 = (B * i) // L
+        b1 = (B * (i + 1)) // L
+        nb = b1 - b0
+        strm = main if i == 0 else torch.cuda.Stream(device=dev)
+        ln = dict(sl=slice(b0, b1), stream=strm,
+                  scal=torch.empty(ops.NSCAL, **f32), part=torch.empty(ops.lstm_ntiles(h), nb * N, **f32),
+                  kws=ops.kkt_resgrad_ws(nb, n, m, dev))
+        if f16:  # split planes of H (ping-pong)
+            f16t = dict(dtype=torch.float16, device=dev)
+            ln["H16"] = [torch.zeros(2, nb, N, h, **f16t), torch.empty(2, nb, N, h, **f16t)]
+        lane.append(ln)
+    scal = lane[0]["scal"]
+    timer.stop(tok)
+    if L > 1:  # the lanes start after the scaling and the zero-fills on the main stream
+        ready = main.record_event()
+        for ln in lane:
+            if ln["stream"] is not main:
+                ln["stream"].wait_event(ready)
+    # Lane i starts one residual-matvec later than lane i-1 (it waits for that lane's first KKT
+    # launch).  Started together, the lanes run in lockstep (their cell kernels share the chip
+    # evenly and end together, so their matvecs meet again); staggered, every lane's matvec and
+    # update run while the other lanes' cell kernels run, and the offset persists.  (A high-priority
+    # stream for lane 0 instead measured no better: profiles/r02_lanes.txt.)
+
+    def iterate(ln, t, cur, nxt):
+        sl, sc, part = ln["sl"], ln["scal"], ln["part"]
+        ops.schedule(rho_p, alpha_p, t, out=sc)
+        k = timer.start("k:kkt_resgrad")
+        ops.kkt_resgrad(Qs[sl], As[sl], pv[sl], xs[cur][sl], ys[cur][sl], zs[cur][sl], xvs[cur][sl], sigma, sc,
+                        num_ineq, g=g[sl], ws=ln["kws"])
+        timer.stop(k)
+        if t == 0 and L > 1:
+            ln["kkt0"] = torch.cuda.current_stream(dev).record_event()
+        k = timer.start("k:lstm_cell")
+        if f16:
+            H16 = ln["H16"]
+            ops.lstm_cell_f16x3(H16[cur], C[sl], xvs[cur][sl], g[sl], Upk16, wscale, Wx, Hn16=H16[nxt], Cn=C[sl],
+                                part=part, Hn=Hs[0][sl] if t == T - 1 else None)
+        else:
+            ops.lstm_cell(Hs[cur][sl], C[sl], xvs[cur][sl], g[sl], Upk, Wx, Hn=Hs[nxt][sl], Cn=C[sl], part=part)
+        timer.stop(k)
+        ops.admm_update(n, m, num_ineq, part, b_h, xvs[cur][sl], xs[cur][sl], ys[cur][sl], zs[cur][sl], zlv[sl],
+                        zuv[sl], sc, out=(xvs[nxt][sl], xs[nxt][sl], ys[nxt][sl], zs[nxt][sl]))
 
     cur = 0
     # timed scope = the reference's model() calls (main.py:881-890): with history the per-iteration
@@ -182,19 +263,14 @@ def solve(params, Q, p, A0, zl, zu, num_ineq, num_eq, T, sigma, scaling=True, sc
         nxt = 1 - cur
         if history:
             tok = timer.start("iterations")
-        ops.schedule(rho_p, alpha_p, t, out=scal)
-        k = timer.start("k:kkt_resgrad")
-        ops.kkt_resgrad(Qs, As, pv, xs[cur], ys[cur], zs[cur], xvs[cur], sigma, scal, num_ineq, g=g, ws=kws)
-        timer.stop(k)
-        k = timer.start("k:lstm_cell")
-        if f16:
-            ops.lstm_cell_f16x3(H16s[cur], C, xvs[cur], g, Upk16, wscale, Wx, Hn16=H16s[nxt], Cn=C, part=part,
-                                Hn=Hs[0] if t == T - 1 else None)
+        if L == 1:
+            iterate(lane[0], t, cur, nxt)
         else:
-            ops.lstm_cell(Hs[cur], C, xvs[cur], g, Upk, Wx, Hn=Hs[nxt], Cn=C, part=part)
-        timer.stop(k)
-        ops.admm_update(n, m, num_ineq, part, b_h, xvs[cur], xs[cur], ys[cur], zs[cur], zlv, zuv, scal,
-                        out=(xvs[nxt], xs[nxt], ys[nxt], zs[nxt]))
+            for i, ln in enumerate(lane):  # enqueued round-robin; the lanes' streams run concurrently
+                with torch.cuda.stream(ln["stream"]):
+                    if t == 0 and i > 0:
+                        ln["stream"].wait_event(lane[i - 1]["kkt0"])
+                    iterate(ln, t, cur, nxt)
         if history:  # main.py:949-957 on unscaled data; kept on device
             timer.stop(tok)
             htok = timer.start("hist:metrics")
@@ -213,6 +289,9 @@ def solve(params, Q, p, A0, zl, zu, num_ineq, num_eq, T, sigma, scaling=True, sc
                 iter_hook(t, ux, uy, uz)
             timer.stop(htok)
         cur = nxt
+    for ln in lane:  # join: everything after (and every buffer's release) orders after the lanes
+        if ln["stream"] is not main:
+            main.wait_stream(ln["stream"])
     if not history:
         timer.stop(tok)
 
@@ -223,8 +302,10 @@ def solve(params, Q, p, A0, zl, zu, num_ineq, num_eq, T, sigma, scaling=True, sc
         x, y, z = xs[cur], ys[cur], zs[cur]
     timer.stop(tok)
 
+    tok = timer.start("metrics")
     obj, pr, du = _metrics(Q, p, A0, Qs, ps, As, D, E, c, x, y, z, xs[cur], ys[cur], zs[cur],
                            keep_unscaled or not scaling)
+    timer.stop(tok)
     out = dict(x=x.unsqueeze(-1), y=y.unsqueeze(-1), z=z.unsqueeze(-1), xv=xvs[cur].unsqueeze(-1),
                H=Hs[0] if f16 else Hs[cur], C=C, x_scaled=xs[cur].unsqueeze(-1), y_scaled=ys[cur].unsqueeze(-1),
                z_scaled=zs[cur].unsqueeze(-1), obj=obj, primal=pr, dual=du, scal=scal,
