@@ -2,6 +2,7 @@
 // recompute in the training backward (train.hip).  See lstm.hip for the tiling.
 #pragma once
 #include "common.h"
+#include <type_traits>
 
 namespace iadmm {
 
@@ -335,16 +336,210 @@ IADMM_DEV void mainloop_dma(const float* __restrict__ Abase, int na_valid, int l
 template <int NA>
 constexpr int dma_ring_floats() { return kStages * (NA * 32 * kBKd + kStageB) + ((NA * 2) % 4 ? 256 : 0); }
 
+template <int S>
+struct Stage { static constexpr int value = S; };
+
+// mainloop_dma<true, NA> for K % 16 == 0 with no VALU work in the loop: same products, same
+// accumulation order, so bitwise the same result.  On gfx950 the fp32 MFMA runs on the VALU
+// datapath (tools/mfma_valu_probe.hip: a VALU instruction beside v_mfma_f32_32x32x2_f32 is never
+// hidden, ~5 cycles each), so the generic loop's 18 VALU per chunk (DMA offsets with per-lane
+// tail checks, stage-relative fragment addresses) cost ~2.4 % of the MFMA time.  Here
+//   * every DMA piece keeps a loop-invariant per-lane voffset; the chunk's position goes into the
+//     scalar soffset and the LDS stage into M0 (SALU only).  K % 16 == 0 and K <= ldb mean no k
+//     tail; rows past nb_valid still read zero from the descriptor's range check; chunks past the
+//     end are issued through an empty descriptor (num_records 0: zeros, no traffic);
+//   * the loop is unrolled by the 3 ring stages, so every fragment address is a loop-invariant
+//     lane base + an immediate offset (ring <= 72 KiB: the 16-bit ds_read offset reaches it).
+template <int NA, class BeforeLast>
+IADMM_DEV void mainloop_dma_k16(const float* __restrict__ Abase, const float* __restrict__ Bbase, int64_t nb_valid,
+                                int ldb, int K, float* ring, floatx16 (&acc)[NA][2], int tid, int wave, int jl,
+                                int hf, BeforeLast&& before_last) {
+  static_assert(NA == 4 || NA == 5, "A tile = 4 or 5 blocks of 32 rows");
+  constexpr int AROWS = NA * 32;
+  constexpr int STA = AROWS * kBKd;
+  constexpr int ST = STA + kStageB;
+  constexpr int NPA = NA * 2;
+  constexpr int APW = (NPA + 3) / 4;
+  // acc is not zeroed with moves: chunk 0's first MFMA of each accumulator takes an inline-zero C
+  // operand instead (128 fewer VALU writes per tile; chunk 0 is peeled for that)
+
+  const int lane = tid & 63;
+  const int nk = K / kBKd;
+  const int nkc32 = (K + kBK - 1) / kBK;
+  const int64_t nbv = nb_valid < 256 ? nb_valid : 256;
+  const __amdgpu_buffer_rsrc_t hrs = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float*>(Bbase), 0, (int)(nbv * ldb * 4), 0x00020000);
+  const __amdgpu_buffer_rsrc_t urs = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float*>(Abase), 0, nkc32 * AROWS * kBK * 4, 0x00020000);
+  const __amdgpu_buffer_rsrc_t zrs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(Abase), 0, 0, 0x00020000);
+
+  const int prow = lane >> 2, pslot = lane & 3;
+  unsigned aoff[APW], boff[4];
+#pragma unroll
+  for (int i = 0; i < APW; ++i) {
+    const int row = (wave + 4 * i) * 16 + prow;
+    aoff[i] = (unsigned)(row * kBK + 4 * (pslot ^ ((row >> 2) & 3))) * 4u;
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int row = (wave * 4 + i) * 16 + prow;
+    boff[i] = (unsigned)(row * ldb + 4 * (pslot ^ ((row >> 2) & 3))) * 4u;
+  }
+  auto issue = [&](int kc, auto S) {
+    constexpr int s = decltype(S)::value;
+    const bool live = kc < nk;
+    const __amdgpu_buffer_rsrc_t ua = live ? urs : zrs, hb = live ? hrs : zrs;
+    const int sa_off = ((kc >> 1) * AROWS * kBK + (kc & 1) * kBKd) * 4;
+    const int sb_off = kc * kBKd * 4;
+    float* sa = ring + s * ST;
+    float* sb = sa + STA;
+#pragma unroll
+    for (int i = 0; i < APW; ++i) {
+      const int p = wave + 4 * i;
+      const bool real = NPA % 4 == 0 || p < NPA;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(real ? ua : zrs, (lds_void*)(real ? sa + p * 256 : ring + kStages * ST),
+                                               16, aoff[i], sa_off, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(hb, (lds_void*)(sb + (wave * 4 + i) * 256), 16, boff[i], sb_off, 0, 0);
+  };
+  const int sw = (jl >> 2) & 3;
+  // lane offsets of the fragment reads; laundered through an empty asm once per chunk so the
+  // compiler cannot hoist (lane offset + stage/gate constant) sums out of the loop as separate
+  // registers: each read stays "lane offset + immediate"
+  // LDS byte addresses (ring base folded in) of the fragment reads
+  typedef __attribute__((address_space(3))) float lds_float;
+  const unsigned rb = (unsigned)(uintptr_t)(lds_float*)ring;
+  unsigned aoffG[2] = {rb + (jl * kBKd + 4 * ((0 + hf) ^ sw)) * 4u, rb + (jl * kBKd + 4 * ((2 + hf) ^ sw)) * 4u};
+  unsigned boffG[2] = {rb + (STA + (wave * 64 + jl) * kBKd + 4 * ((0 + hf) ^ sw)) * 4u,
+                       rb + (STA + (wave * 64 + jl) * kBKd + 4 * ((2 + hf) ^ sw)) * 4u};
+  auto launder = [&] {
+    asm volatile("" : "+v"(aoffG[0]), "+v"(aoffG[1]), "+v"(boffG[0]), "+v"(boffG[1]));
+  };
+  typedef float f4v __attribute__((ext_vector_type(4)));
+  typedef __attribute__((address_space(3))) const f4v lds_f4;
+  auto ld = [](unsigned addr) -> float4 {
+    const f4v v = *(lds_f4*)(uintptr_t)addr;
+    return make_float4(v.x, v.y, v.z, v.w);
+  };
+  float4 fa0[NA], fb0[2], fa1[NA], fb1[2];
+  auto frag = [&](auto S, int G, float4 (&fa)[NA], float4 (&fb)[2]) {
+    constexpr unsigned so = decltype(S)::value * ST * 4u;
+#pragma unroll
+    for (int g = 0; g < NA; ++g) fa[g] = ld(aoffG[G] + so + g * 32 * kBKd * 4u);
+#pragma unroll
+    for (int r = 0; r < 2; ++r) fb[r] = ld(boffG[G] + so + r * 32 * kBKd * 4u);
+  };
+  auto mma = [&](const float4 (&fa)[NA], const float4 (&fb)[2], auto First) {
+    constexpr bool first = decltype(First)::value;
+    const floatx16 zero = {};
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+#pragma unroll
+      for (int g = 0; g < NA; ++g)
+#pragma unroll
+        for (int r = 0; r < 2; ++r)
+          acc[g][r] = __builtin_amdgcn_mfma_f32_32x32x2f32(get4(fa[g], s), get4(fb[r], s),
+                                                           (first && s == 0) ? zero : acc[g][r], 0, 0, 0);
+  };
+  using No = std::integral_constant<bool, false>;
+  using Yes = std::integral_constant<bool, true>;
+  constexpr int NRD = NA + 2;
+  constexpr int NMF = 8 * NA;
+  // one chunk kc (stage S = kc % 3): the schedule of mainloop_dma's loop body
+  auto step = [&](int kc, auto S, auto First) {
+    constexpr int s = decltype(S)::value;
+    launder();
+    frag(S, 1, fa1, fb1);
+    mma(fa0, fb0, First);
+#pragma unroll
+    for (int i = 0; i < NRD; ++i) {
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+    }
+    __builtin_amdgcn_sched_group_barrier(0x008, NMF - NRD, 0);
+    __builtin_amdgcn_sched_barrier(0);
+    vm_wait<0>();
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    issue(kc + 2, Stage<(s + 2) % 3>{});
+    frag(Stage<(s + 1) % 3>{}, 0, fa0, fb0);
+    mma(fa1, fb1, No{});
+#pragma unroll
+    for (int i = 0; i < APW + 4; ++i) {
+      __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < NRD; ++i) {
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+    }
+    __builtin_amdgcn_sched_group_barrier(0x008, NMF - NRD - APW - 4, 0);
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  auto last = [&](auto S, auto First) {
+    frag(S, 1, fa1, fb1);
+    before_last();
+    __builtin_amdgcn_sched_barrier(0);
+    mma(fa0, fb0, First);
+    mma(fa1, fb1, No{});
+    __builtin_amdgcn_sched_barrier(0);  // nothing of the caller's epilogue moves above these MFMAs
+  };
+
+  // Stage numbering is rotated so the peeled last chunk always lands in stage 0 (one copy of the
+  // epilogue-operand prefetch): chunk kc uses stage (kc + d) % 3; the r = (nk - 1) % 3 head chunks
+  // run before the 3-way unrolled loop.
+  const int r = (nk - 1) % 3;
+  const int d = (3 - r) % 3;
+  if (d == 0) { issue(0, Stage<0>{}); issue(1, Stage<1>{}); }  // chunk 1 past the end when nk == 1:
+  else if (d == 1) { issue(0, Stage<1>{}); issue(1, Stage<2>{}); }  // zeros into a stage nobody reads
+  else { issue(0, Stage<2>{}); issue(1, Stage<0>{}); }
+  vm_wait<APW + 4>();
+  __builtin_amdgcn_s_barrier();
+  if (d == 0) frag(Stage<0>{}, 0, fa0, fb0);
+  else if (d == 1) frag(Stage<1>{}, 0, fa0, fb0);
+  else frag(Stage<2>{}, 0, fa0, fb0);
+  int kc;
+  if (nk == 1) {
+    last(Stage<0>{}, Yes{});
+    return;
+  }
+  if (r == 2) {
+    step(0, Stage<1>{}, Yes{});
+    step(1, Stage<2>{}, No{});
+    kc = 2;
+  } else if (r == 1) {
+    step(0, Stage<2>{}, Yes{});
+    kc = 1;
+  } else {  // nk - 1 = 3, 6, ...
+    step(0, Stage<0>{}, Yes{});
+    step(1, Stage<1>{}, No{});
+    step(2, Stage<2>{}, No{});
+    kc = 3;
+  }
+  for (; kc < nk - 1; kc += 3) {
+    step(kc, Stage<0>{}, No{});
+    step(kc + 1, Stage<1>{}, No{});
+    step(kc + 2, Stage<2>{}, No{});
+  }
+  last(Stage<0>{}, No{});
+}
+
 // The cell's instance: A = the packed gate weights of hidden tile jt, B = the H panel of rows
-// [rbase, rbase + 256).
-template <class BeforeLast>
+// [rbase, rbase + 256).  K16: h % 16 == 0 (mainloop_dma_k16).
+template <bool K16, class BeforeLast>
 IADMM_DEV void cell_mainloop_dma(const float* __restrict__ H, int64_t M, int h, int nkc32,
                                  const float* __restrict__ Ubase, int64_t rbase, float* ring,
                                  floatx16 (&acc)[4][2], int tid, int wave, int jl, int hf,
                                  BeforeLast&& before_last) {
   (void)nkc32;
-  mainloop_dma<true>(Ubase, 128, kBK, H + rbase * h, M - rbase, h, h, ring, acc, tid, wave, jl, hf,
-                     before_last);
+  if constexpr (K16)
+    mainloop_dma_k16<4>(Ubase, H + rbase * h, M - rbase, h, h, ring, acc, tid, wave, jl, hf, before_last);
+  else
+    mainloop_dma<true>(Ubase, 128, kBK, H + rbase * h, M - rbase, h, h, ring, acc, tid, wave, jl, hf,
+                       before_last);
 }
 
 // The fused cell epilogue: gates, C' = I U + F C, H' = O tanh(C'), projection partial, from the
@@ -425,8 +620,8 @@ IADMM_DEV void cell_epi_compute(const CellArgsT& a, floatx16 (&acc)[4][2], const
         float2v pre[4];
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
-          const float2v xw = in0 * fld(3 * g) + in1 * fld(3 * g + 1);
-          pre[g] = (xw + float2v{acc[g][r][q], acc[g][r][q + 1]}) + fld(3 * g + 2);
+          pre[g] = cell_pre2(in0, in1, float2v{acc[g][r][q], acc[g][r][q + 1]}, fld(3 * g), fld(3 * g + 1),
+                             fld(3 * g + 2));
         }
         const float2v ig = sigmoid_cell2(pre[0]), fg = sigmoid_cell2(pre[1]), og = sigmoid_cell2(pre[2]);
         const float2v ug = tanh_cell2(pre[3]);
@@ -459,6 +654,121 @@ IADMM_DEV void cell_epi_compute(const CellArgsT& a, floatx16 (&acc)[4][2], const
     float gsum = gs.x + gs.y;
     gsum += __shfl_xor(gsum, 32, 64);
     if (hf == 0 && rok) a.part[(int64_t)jt * M + R] = gsum;
+  }
+}
+
+// The DMA kernel's epilogue on buffer loads/stores (h % 4 == 0).  Every global access of the
+// epilogue goes through a descriptor based at the workgroup's row panel whose range ends at its last
+// valid row: rows past M read 0 / are dropped by the range check (no exec-mask branches, no
+// zeroing moves), and each lane needs one 32-bit offset per row block, the unit groups (qq) being
+// immediate offsets -- a fraction of the 64-bit address VALU of cell_epi_load / cell_epi_compute.
+// (Each VALU instruction here costs the SIMD's fp32-MFMA stream its issue cycles:
+// tools/mfma_valu_probe.hip.)  Same arithmetic as cell_epi_compute: bitwise the same results.
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+struct CellEpiBuf {
+  __amdgpu_buffer_rsrc_t c, cn, hn, xv, g, part;
+  unsigned vo[2];    // bytes: (row block r of the lane, units jt*32 + 4*hf) inside the panel
+  unsigned vr[2];    // bytes: row of the lane inside the panel (xv, g); part: out of range for hf = 1
+  unsigned qadd[4];  // tail hidden tile only: qq*32 B, or out of range past h
+  bool full;         // the hidden tile has all 32 units (uniform)
+  float4 cold[2][4];
+  float in0[2], in1[2];
+};
+
+IADMM_DEV void cell_epi_setup_buf(const CellArgsT& a, int jt, int64_t rbase, int wave, int jl, int hf, CellEpiBuf& e) {
+  const int h = a.h;
+  const int64_t M = a.M;
+  const int nvalid = (int)((M - rbase) < kRows ? (M - rbase) : kRows);
+  const int64_t pan = rbase * h;
+  e.c = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.C + pan), 0, nvalid * h * 4, 0x00020000);
+  e.cn = __builtin_amdgcn_make_buffer_rsrc(a.Cn + pan, 0, nvalid * h * 4, 0x00020000);
+  e.hn = __builtin_amdgcn_make_buffer_rsrc(a.Hn + pan, 0, nvalid * h * 4, 0x00020000);
+  e.xv = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.xv + rbase), 0, nvalid * 4, 0x00020000);
+  e.g = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.g + rbase), 0, nvalid * 4, 0x00020000);
+  e.part = __builtin_amdgcn_make_buffer_rsrc(a.part + (int64_t)jt * M + rbase, 0, nvalid * 4, 0x00020000);
+#pragma unroll
+  for (int r = 0; r < 2; ++r) {
+    const unsigned row = (unsigned)(wave * 64 + r * 32 + jl);
+    e.vo[r] = (row * (unsigned)h + (unsigned)(jt * kJT + 4 * hf)) * 4u;
+    e.vr[r] = row * 4u;
+  }
+  e.full = (jt + 1) * kJT <= h;
+  if (!e.full) {
+#pragma unroll
+    for (int qq = 0; qq < 4; ++qq) e.qadd[qq] = jt * kJT + 8 * qq + 4 * hf < h ? 32u * qq : 0x80000000u;
+  }
+}
+
+IADMM_DEV float4 u2f4(u32x4 v) {
+  return make_float4(__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z), __uint_as_float(v.w));
+}
+IADMM_DEV u32x4 f42u(float4 v) {
+  return u32x4{__float_as_uint(v.x), __float_as_uint(v.y), __float_as_uint(v.z), __float_as_uint(v.w)};
+}
+
+IADMM_DEV void cell_epi_load_buf(CellEpiBuf& e) {
+#pragma unroll
+  for (int r = 0; r < 2; ++r) {
+    e.in0[r] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(e.xv, e.vr[r], 0, 0));
+    e.in1[r] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(e.g, e.vr[r], 0, 0));
+    if (e.full) {
+#pragma unroll
+      for (int qq = 0; qq < 4; ++qq) e.cold[r][qq] = u2f4(__builtin_amdgcn_raw_buffer_load_b128(e.c, e.vo[r] + 32u * qq, 0, 0));
+    } else {
+#pragma unroll
+      for (int qq = 0; qq < 4; ++qq) e.cold[r][qq] = u2f4(__builtin_amdgcn_raw_buffer_load_b128(e.c, e.vo[r] + e.qadd[qq], 0, 0));
+    }
+  }
+}
+
+template <int DIAG = 0>
+IADMM_DEV void cell_epi_compute_buf(floatx16 (&acc)[4][2], const float* sWp, int hf, CellEpiBuf& e) {
+#pragma unroll
+  for (int r = 0; r < 2; ++r) {
+    const float2v in0 = splat2(e.in0[r]), in1 = splat2(e.in1[r]);
+    float2v gs = splat2(0.f);
+#pragma unroll
+    for (int qq = 0; qq < 4; ++qq) {
+      __builtin_amdgcn_sched_barrier(0);  // one (rows, 4 units) group at a time: bounded live range
+      const int jj0 = 8 * qq + 4 * hf;
+      const float4 cold = e.cold[r][qq];
+      float4 cnew, hnew;
+#pragma unroll
+      for (int pp = 0; pp < 2; ++pp) {
+        const float4* wp = reinterpret_cast<const float4*>(sWp + ((jj0 >> 1) + pp) * 32);
+        float4 w4[7];
+#pragma unroll
+        for (int i = 0; i < 7; ++i) w4[i] = wp[i];
+        auto fld = [&](int f) -> float2v {
+          const float4& t = w4[f >> 1];
+          return (f & 1) ? float2v{t.z, t.w} : float2v{t.x, t.y};
+        };
+        const int q = qq * 4 + 2 * pp;
+        float2v pre[4];
+#pragma unroll
+        for (int g = 0; g < 4; ++g)
+          pre[g] = cell_pre2(in0, in1, float2v{acc[g][r][q], acc[g][r][q + 1]}, fld(3 * g), fld(3 * g + 1),
+                             fld(3 * g + 2));
+        const float2v ig = sigmoid_cell2(pre[0]), fg = sigmoid_cell2(pre[1]), og = sigmoid_cell2(pre[2]);
+        const float2v ug = tanh_cell2(pre[3]);
+        const float2v cv = pp ? float2v{cold.z, cold.w} : float2v{cold.x, cold.y};
+        const float2v c2 = ig * ug + fg * cv;
+        const float2v h2 = og * tanh_cell2(c2);
+        gs = fma2(h2, fld(12), gs);
+        if (pp == 0) { cnew.x = c2.x; cnew.y = c2.y; hnew.x = h2.x; hnew.y = h2.y; }
+        else         { cnew.z = c2.x; cnew.w = c2.y; hnew.z = h2.x; hnew.w = h2.y; }
+      }
+      if (DIAG == 2) {  // timing diagnostic: no H'/C' stores (keep the values alive)
+        gs.x += cnew.x + cnew.y + cnew.z + cnew.w;
+      } else {
+        const unsigned o = e.vo[r] + (e.full ? 32u * qq : e.qadd[qq]);
+        __builtin_amdgcn_raw_buffer_store_b128(f42u(cnew), e.cn, o, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b128(f42u(hnew), e.hn, o, 0, 0);
+      }
+    }
+    float gsum = gs.x + gs.y;
+    gsum += __shfl_xor(gsum, 32, 64);
+    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(gsum), e.part, hf ? 0x80000000u : e.vr[r], 0, 0);
   }
 }
 
@@ -497,14 +807,15 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void cell_fwd_kernel(Cell
 }
 
 
-// Forward cell kernel on the LDS-DMA main loop (VEC only: h % 4 == 0, 16-B aligned rows).
+// Forward cell kernel on the LDS-DMA main loop (VEC only: h % 4 == 0, 16-B aligned rows); K16:
+// h % 16 == 0, the VALU-free loop (mainloop_dma_k16).
 // Dynamic LDS: kRingFloats + kWxF*kJT floats (74 KiB) -> 2 workgroups per CU.
 // DIAG (timing tools only): 1 = skip the epilogue (main-loop cost); 2 = epilogue without the
 // H'/C' stores; 3 = epilogue without the C / xv / g loads.
 // DIAG 4: as 0, plus s_memtime stamps (kernel start, main loop end, epilogue operands landed,
 // epilogue end) of wave 0 of every workgroup into a.part[njt * M ...]; 5: same without the H'/C'
 // stores -- diagnostic builds only (tools/cellbench).
-template <int DIAG = 0>
+template <int DIAG = 0, bool K16 = false>
 __global__ __launch_bounds__(256, 2) void cell_fwd_dma_kernel(CellArgsT a) {
   extern __shared__ __attribute__((aligned(16))) float dsm[];
   uint64_t t_start = 0, t_ml = 0;
@@ -518,9 +829,14 @@ __global__ __launch_bounds__(256, 2) void cell_fwd_dma_kernel(CellArgsT a) {
   const int jl = lane & 31, hf = lane >> 5;
   const int64_t rbase = (int64_t)rt * kRows;
   cell_fill_wpairs(a.Wx, jt, sW, tid, 256);
+  // sW visible to every wave.  Here rather than after the main loop: a fence there would wait
+  // (vmcnt) for the epilogue operands prefetched behind the last chunk, and the compiler may sink
+  // the last chunk's MFMAs below the barrier, exposing that load latency.
+  __syncthreads();
   floatx16 acc[4][2];
-  CellEpiIn ei;
-  cell_mainloop_dma(a.H, a.M, a.h, a.nkc32, a.Upk + (int64_t)jt * a.nkc32 * 128 * kBK, rbase, ring, acc,
+  CellEpiBuf ei;
+  cell_epi_setup_buf(a, jt, rbase, wave, jl, hf, ei);
+  cell_mainloop_dma<K16>(a.H, a.M, a.h, a.nkc32, a.Upk + (int64_t)jt * a.nkc32 * 128 * kBK, rbase, ring, acc,
                     tid, wave, jl, hf, [&] {
                       if constexpr (DIAG == 3) {
 #pragma unroll
@@ -530,7 +846,7 @@ __global__ __launch_bounds__(256, 2) void cell_fwd_dma_kernel(CellArgsT a) {
                           for (int qq = 0; qq < 4; ++qq) ei.cold[r][qq] = make_float4(0.1f, 0.2f, 0.3f, 0.4f);
                         }
                       } else {
-                        cell_epi_load<true>(a, jt, rbase, wave, jl, hf, ei);
+                        cell_epi_load_buf(ei);
                       }
                     });
   if constexpr (DIAG == 1) {
@@ -544,14 +860,16 @@ __global__ __launch_bounds__(256, 2) void cell_fwd_dma_kernel(CellArgsT a) {
     a.part[(int64_t)blockIdx.x * 256 + tid] = t;
     return;
   }
-  __syncthreads();  // sW visible (written before the main loop)
+#ifdef IADMM_EPI_PRIO
+  __builtin_amdgcn_s_setprio(IADMM_EPI_PRIO);  // variant study: epilogue priority
+#endif
   uint64_t t_c = 0;
   if constexpr (DIAG >= 4) {
     t_ml = __builtin_amdgcn_s_memtime();
     vm_wait<0>();  // the prefetched epilogue operands
     t_c = __builtin_amdgcn_s_memtime();
   }
-  cell_epi_compute<true, DIAG == 4 ? 0 : (DIAG == 5 ? 2 : DIAG)>(a, acc, sW, jt, rbase, wave, jl, hf, ei);
+  cell_epi_compute_buf<DIAG == 4 ? 0 : (DIAG == 5 ? 2 : DIAG)>(acc, sW, hf, ei);
   if constexpr (DIAG >= 4) {
     const uint64_t t_end = __builtin_amdgcn_s_memtime();
     if (tid == 0) {

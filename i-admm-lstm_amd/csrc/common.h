@@ -32,71 +32,71 @@ IADMM_DEV float tmax(float a, float b) { return (a != a || b != b) ? __builtin_n
 
 IADMM_DEV float sigmoidf_(float x) { return 1.0f / (1.0f + expf(-x)); }
 
-// LSTM-cell transcendentals (branch-free, <= 3.1 ulp; tools/mathcheck.hip measures them against
-// fp64).  Each has a scalar form and a packed two-lane form (v_pk_*_f32 for everything but the
-// v_exp/v_rcp transcendentals) built from the SAME operation sequence, so both give bitwise
+// LSTM-cell transcendentals, branch-free (tools/mathcheck.hip measures them against fp64).  Each
+// has a scalar form and a packed two-lane form (v_pk_*_f32 for everything but the v_exp/v_rcp
+// transcendentals and the clamp) built from the SAME operation sequence, so both give bitwise
 // identical results; the cell epilogue runs the packed form, the training recompute the scalar.
-//   exp:     e^y = 2^th * 2^tl with th + tl = y log2(e) split exactly by an fma, 2^th on v_exp_f32
-//            and 2^tl ~ 1 + tl ln2 (|tl| < 2^-10, so the dropped terms are < 2^-22 relative)
-//   sigmoid: 1 / (1 + e^-x) with the hardware reciprocal
-//   tanh:    odd minimax polynomial x + x^3 P(x^2) on |x| < 0.625 (approximation error 4.5e-9
-//            relative), 1 - 2/(e^{2|x|} + 1) above (no cancellation there: 2/(e+1) <= 0.45)
+//   sigmoid: 1 / (1 + 2^(-x log2 e)) on v_exp_f32 + v_rcp_f32 (relative error ~|x| 2^-24: no
+//            cancellation anywhere)
+//   tanh:    x P(x^2) / Q(x^2), P of degree 6, Q of degree 3 in x^2, on |x| clamped to 7.9053
+//            (where fp32 tanh reaches 1 within 5 ulp); coefficients fitted here for minimal relative
+//            error (5e-9 in exact arithmetic, <= ~6 ulp evaluated in fp32): relative accuracy down
+//            to 0 (small LSTM states), no exp, no select
+// The sigmoid needs no clamp: 2^(+inf) = inf -> rcp = 0, 2^(-inf) = 0 -> rcp(1) = 1, so it
+// saturates to 0 / 1 like torch and NaN propagates; tanh saturates through its clamp.
+// Why so lean: on gfx950 v_mfma_f32_32x32x2_f32 runs on the fp32 VALU datapath, so every VALU
+// cycle of the epilogue is a cycle the SIMD's matrix work stalls (tools/mfma_valu_probe.hip,
+// profiles/r02_mfma_valu_probe.txt).  The r01 forms (Cody-Waite exp with a v_med3 clamp, tanh as a
+// polynomial/exp select with |x| and copysign) spent ~2x the VALU cycles.
 typedef float float2v __attribute__((ext_vector_type(2)));
-constexpr float kL2E = 1.44269502f;           // fp32(log2 e)
-constexpr float kL2E_LO = 1.925963033e-08f;   // log2(e) - kL2E
-constexpr float kLN2 = 0.693147181f;
-constexpr float kTh4 = -0.0057040372917676625f, kTh3 = 0.020637863933015994f, kTh2 = -0.05373916009365762f,
-                kTh1 = 0.13331431844163766f, kTh0 = -0.3333328129024227f;
+constexpr float kNL2E = -1.44269502f;          // -fp32(log2 e)
+constexpr float kTanhClamp = 7.90531110763549805f;
+constexpr float kTp1 = 0.1313343644142151f, kTp2 = 0.0031596473418176174f, kTp3 = 1.1755176274164114e-05f,
+                kTp4 = -2.281726452224575e-08f, kTp5 = 6.643676581097324e-11f, kTp6 = -1.241359852367438e-13f;
+constexpr float kTq1 = 0.4646677076816559f, kTq2 = 0.024715565145015717f, kTq3 = 0.00026282211183570325f;
 
-// y is clamped to [-87, 88] first (v_med3): e^y stays finite, so the fma correction never meets
-// inf (inf * negative + inf = NaN) and +-inf inputs give sigmoid 0 / 1 like torch; beyond the clamp
-// the sigmoid differs from the exact value by < 1e-38.
-IADMM_DEV float exp_cell(float y) {
-  y = __builtin_amdgcn_fmed3f(y, -87.0f, 88.0f);
-  const float th = y * kL2E;
-  float tl = fmaf(y, kL2E, -th);
-  tl = fmaf(y, kL2E_LO, tl);
-  const float e = __builtin_amdgcn_exp2f(th);
-  return fmaf(e, tl * kLN2, e);
-}
-IADMM_DEV float sigmoid_cell(float x) { return __builtin_amdgcn_rcpf(1.0f + exp_cell(-x)); }
+IADMM_DEV float sigmoid_cell(float x) { return __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(x * kNL2E)); }
 IADMM_DEV float tanh_cell(float x) {
+  x = __builtin_amdgcn_fmed3f(x, -kTanhClamp, kTanhClamp);
   const float s = x * x;
-  float p = fmaf(s, kTh4, kTh3);
-  p = fmaf(s, p, kTh2);
-  p = fmaf(s, p, kTh1);
-  p = fmaf(s, p, kTh0);
-  const float small = fmaf(x * s, p, x);
-  const float ax = fabsf(x);
-  const float e = __builtin_amdgcn_exp2f((ax + ax) * kL2E);
-  const float big = fmaf(-2.0f, __builtin_amdgcn_rcpf(e + 1.0f), 1.0f);
-  return ax < 0.625f ? small : copysignf(big, x);
+  float p = fmaf(s, kTp6, kTp5);
+  p = fmaf(s, p, kTp4);
+  p = fmaf(s, p, kTp3);
+  p = fmaf(s, p, kTp2);
+  p = fmaf(s, p, kTp1);
+  p = fmaf(s, p, 1.0f);
+  float q = fmaf(s, kTq3, kTq2);
+  q = fmaf(s, q, kTq1);
+  q = fmaf(s, q, 1.0f);
+  return (x * p) * __builtin_amdgcn_rcpf(q);
+}
+// Gate pre-activation: (b + in0 w0 + in1 w1) + acc, i.e. inputs @ W + H @ U + b
+// (models/lstm.py:74-77) with the two-term input product on fmas.
+IADMM_DEV float cell_pre(float in0, float in1, float acc, float w0, float w1, float b) {
+  return fmaf(in1, w1, fmaf(in0, w0, b)) + acc;
 }
 
 IADMM_DEV float2v fma2(float2v a, float2v b, float2v c) { return __builtin_elementwise_fma(a, b, c); }
 IADMM_DEV float2v splat2(float v) { return float2v{v, v}; }
-IADMM_DEV float2v exp_cell2(float2v y) {
-  y = float2v{__builtin_amdgcn_fmed3f(y.x, -87.0f, 88.0f), __builtin_amdgcn_fmed3f(y.y, -87.0f, 88.0f)};
-  const float2v th = y * splat2(kL2E);
-  float2v tl = fma2(y, splat2(kL2E), -th);
-  tl = fma2(y, splat2(kL2E_LO), tl);
-  const float2v e = float2v{__builtin_amdgcn_exp2f(th.x), __builtin_amdgcn_exp2f(th.y)};
-  return fma2(e, tl * splat2(kLN2), e);
-}
+IADMM_DEV float2v exp2_2(float2v y) { return float2v{__builtin_amdgcn_exp2f(y.x), __builtin_amdgcn_exp2f(y.y)}; }
 IADMM_DEV float2v rcp2(float2v d) { return float2v{__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)}; }
-IADMM_DEV float2v sigmoid_cell2(float2v x) { return rcp2(splat2(1.0f) + exp_cell2(-x)); }
+IADMM_DEV float2v sigmoid_cell2(float2v x) { return rcp2(splat2(1.0f) + exp2_2(x * splat2(kNL2E))); }
 IADMM_DEV float2v tanh_cell2(float2v x) {
+  x = float2v{__builtin_amdgcn_fmed3f(x.x, -kTanhClamp, kTanhClamp), __builtin_amdgcn_fmed3f(x.y, -kTanhClamp, kTanhClamp)};
   const float2v s = x * x;
-  float2v p = fma2(s, splat2(kTh4), splat2(kTh3));
-  p = fma2(s, p, splat2(kTh2));
-  p = fma2(s, p, splat2(kTh1));
-  p = fma2(s, p, splat2(kTh0));
-  const float2v small = fma2(x * s, p, x);
-  const float2v ax = float2v{fabsf(x.x), fabsf(x.y)};
-  const float2v t = (ax + ax) * splat2(kL2E);
-  const float2v e = float2v{__builtin_amdgcn_exp2f(t.x), __builtin_amdgcn_exp2f(t.y)};
-  const float2v big = fma2(splat2(-2.0f), rcp2(e + splat2(1.0f)), splat2(1.0f));
-  return float2v{ax.x < 0.625f ? small.x : copysignf(big.x, x.x), ax.y < 0.625f ? small.y : copysignf(big.y, x.y)};
+  float2v p = fma2(s, splat2(kTp6), splat2(kTp5));
+  p = fma2(s, p, splat2(kTp4));
+  p = fma2(s, p, splat2(kTp3));
+  p = fma2(s, p, splat2(kTp2));
+  p = fma2(s, p, splat2(kTp1));
+  p = fma2(s, p, splat2(1.0f));
+  float2v q = fma2(s, splat2(kTq3), splat2(kTq2));
+  q = fma2(s, q, splat2(kTq1));
+  q = fma2(s, q, splat2(1.0f));
+  return (x * p) * rcp2(q);
+}
+IADMM_DEV float2v cell_pre2(float2v in0, float2v in1, float2v acc, float2v w0, float2v w1, float2v b) {
+  return fma2(in1, w1, fma2(in0, w0, b)) + acc;
 }
 
 IADMM_DEV float get4(const float4& v, int e) {

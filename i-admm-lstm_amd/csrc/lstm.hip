@@ -109,8 +109,13 @@ extern "C" int iadmm_lstm_cell_fwd(int64_t M, int64_t h, const float* H, const f
   const dim3 grid((unsigned)(nrt * njt));
   if (vec) {
     // LDS-DMA main loop (cell_tile.h cell_mainloop_dma): 74 KiB of dynamic LDS per workgroup
-    IADMM_ALLOW_LDS(cell_fwd_dma_kernel<0>, kDmaLdsBytes);
-    hipLaunchKernelGGL((cell_fwd_dma_kernel<0>), grid, dim3(256), kDmaLdsBytes, (hipStream_t)stream, a);
+    if (h % kBKd == 0) {  // no K tail: the VALU-free loop (cell_tile.h mainloop_dma_k16)
+      IADMM_ALLOW_LDS((cell_fwd_dma_kernel<0, true>), kDmaLdsBytes);
+      hipLaunchKernelGGL((cell_fwd_dma_kernel<0, true>), grid, dim3(256), kDmaLdsBytes, (hipStream_t)stream, a);
+    } else {
+      IADMM_ALLOW_LDS((cell_fwd_dma_kernel<0, false>), kDmaLdsBytes);
+      hipLaunchKernelGGL((cell_fwd_dma_kernel<0, false>), grid, dim3(256), kDmaLdsBytes, (hipStream_t)stream, a);
+    }
   } else
     hipLaunchKernelGGL((cell_fwd_kernel<false, 4, 0>), grid, dim3(256), 0, (hipStream_t)stream, a);
   IADMM_CHECK_LAUNCH();

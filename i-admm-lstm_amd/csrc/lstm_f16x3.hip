@@ -217,8 +217,8 @@ __global__ __launch_bounds__(256, 2) void cell_f16x3_kernel(CellF16x3Args a) {
         float2v pre[4];
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
-          const float2v xw = in0 * fld(3 * g) + in1 * fld(3 * g + 1);
-          pre[g] = (xw + float2v{acc[g][r][q], acc[g][r][q + 1]} * splat2(inv)) + fld(3 * g + 2);
+          pre[g] = cell_pre2(in0, in1, float2v{acc[g][r][q], acc[g][r][q + 1]} * splat2(inv), fld(3 * g),
+                             fld(3 * g + 1), fld(3 * g + 2));
         }
         const float2v ig = sigmoid_cell2(pre[0]), fg = sigmoid_cell2(pre[1]), og = sigmoid_cell2(pre[2]);
         const float2v ug = tanh_cell2(pre[3]);

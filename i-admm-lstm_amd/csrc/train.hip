@@ -121,7 +121,7 @@ struct CellBwdArgs {
 constexpr int kCellBwdLdsVec = kRingFloats * 4;
 constexpr int kCellBwdLdsScalar = (128 + kRows) * kLD * 4;
 
-template <bool VEC>
+template <bool VEC, bool K16 = false>
 __global__ __launch_bounds__(256, 2) void lstm_cell_bwd_kernel(CellBwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) float dsm[];
   __shared__ __attribute__((aligned(16))) float sW[kWxF * kJT];
@@ -143,7 +143,7 @@ __global__ __launch_bounds__(256, 2) void lstm_cell_bwd_kernel(CellBwdArgs a) {
   }
   floatx16 acc[4][2];
   if constexpr (VEC) {
-    cell_mainloop_dma(a.H, M, h, a.nkc, a.Upk + (int64_t)jt * a.nkc * 128 * kBK, rbase, dsm, acc, tid, wave, jl,
+    cell_mainloop_dma<K16>(a.H, M, h, a.nkc, a.Upk + (int64_t)jt * a.nkc * 128 * kBK, rbase, dsm, acc, tid, wave, jl,
                       hf, [] {});
     __syncthreads();  // sW visible (the DMA loop's barriers carry no LDS-write fence)
   } else {
@@ -196,8 +196,8 @@ __global__ __launch_bounds__(256, 2) void lstm_cell_bwd_kernel(CellBwdArgs a) {
           float2v pre[4];
 #pragma unroll
           for (int g = 0; g < 4; ++g) {
-            const float2v xw = in0 * fld(3 * g) + in1 * fld(3 * g + 1);
-            pre[g] = (xw + float2v{acc[g][r][q], acc[g][r][q + 1]}) + fld(3 * g + 2);
+            pre[g] = cell_pre2(in0, in1, float2v{acc[g][r][q], acc[g][r][q + 1]}, fld(3 * g), fld(3 * g + 1),
+                               fld(3 * g + 2));
           }
           const float2v ig = sigmoid_cell2(pre[0]), fg = sigmoid_cell2(pre[1]), og = sigmoid_cell2(pre[2]);
           const float2v ug = tanh_cell2(pre[3]);
@@ -287,8 +287,8 @@ __global__ __launch_bounds__(256, 2) void lstm_cell_bwd_kernel(CellBwdArgs a) {
         float pre[4];
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
-          const float xw = in0 * get4(wv[3 * g], e) + in1 * get4(wv[3 * g + 1], e);
-          pre[g] = (xw + acc[g][r][q]) + get4(wv[3 * g + 2], e);
+          pre[g] = cell_pre(in0, in1, acc[g][r][q], get4(wv[3 * g], e), get4(wv[3 * g + 1], e),
+                            get4(wv[3 * g + 2], e));
         }
         const float ig = sigmoid_cell(pre[0]), fg = sigmoid_cell(pre[1]), og = sigmoid_cell(pre[2]);
         const float ug = tanh_cell(pre[3]);
@@ -567,8 +567,13 @@ extern "C" int iadmm_lstm_cell_bwd(int64_t M, int64_t h, const float* H, const f
                    (!dHn || aligned16(dHn)) && (!dCn || aligned16(dCn));
   const dim3 grid((unsigned)(nrt * njt));
   if (vec) {
-    IADMM_ALLOW_LDS(lstm_cell_bwd_kernel<true>, kCellBwdLdsVec);
-    hipLaunchKernelGGL(lstm_cell_bwd_kernel<true>, grid, dim3(256), kCellBwdLdsVec, (hipStream_t)stream, a);
+    if (h % kBKd == 0) {  // no K tail: the VALU-free DMA loop (cell_tile.h mainloop_dma_k16)
+      IADMM_ALLOW_LDS((lstm_cell_bwd_kernel<true, true>), kCellBwdLdsVec);
+      hipLaunchKernelGGL((lstm_cell_bwd_kernel<true, true>), grid, dim3(256), kCellBwdLdsVec, (hipStream_t)stream, a);
+    } else {
+      IADMM_ALLOW_LDS((lstm_cell_bwd_kernel<true, false>), kCellBwdLdsVec);
+      hipLaunchKernelGGL((lstm_cell_bwd_kernel<true, false>), grid, dim3(256), kCellBwdLdsVec, (hipStream_t)stream, a);
+    }
   } else {
     hipLaunchKernelGGL(lstm_cell_bwd_kernel<false>, grid, dim3(256), kCellBwdLdsScalar, (hipStream_t)stream, a);
   }

@@ -89,15 +89,16 @@ void launch_v(CellArgsT a, int64_t M, hipStream_t s) {
   hipLaunchKernelGGL((cell_fwd_kernel<true, NW, PRIO, BUF>), dim3((unsigned)(nrt * a.njt)), dim3(64 * NW), 0, s, a);
 }
 
-template <int DIAG>
+template <int DIAG, bool K16 = true>
 void launch_dma(CellArgsT a, int64_t M, hipStream_t s) {
   static bool once = [] {
-    CK(hipFuncSetAttribute((const void*)cell_fwd_dma_kernel<DIAG>, hipFuncAttributeMaxDynamicSharedMemorySize, kDmaLdsBytes));
+    CK(hipFuncSetAttribute((const void*)cell_fwd_dma_kernel<DIAG, K16>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                           kDmaLdsBytes));
     return true;
   }();
   (void)once;
   const int64_t nrt = (M + 255) / 256;
-  hipLaunchKernelGGL((cell_fwd_dma_kernel<DIAG>), dim3((unsigned)(nrt * a.njt)), dim3(256), kDmaLdsBytes, s, a);
+  hipLaunchKernelGGL((cell_fwd_dma_kernel<DIAG, K16>), dim3((unsigned)(nrt * a.njt)), dim3(256), kDmaLdsBytes, s, a);
 }
 
 int main(int argc, char** argv) {
@@ -118,11 +119,11 @@ int main(int argc, char** argv) {
   hipLaunchKernelGGL(fill, dim3(4096), dim3(256), 0, 0, Upk, nup, 5u, 0.02f);
   hipLaunchKernelGGL(fill, dim3(256), dim3(256), 0, 0, Wx, nwx, 6u, 0.02f);
   CK(hipDeviceSynchronize());
-  CellArgsT a{M, (int)h, njt, nkc32, H, C, xv, g, Upk, Wx, Hn, Cn, part};
+  CellArgsT a{M, (int)h, njt, nkc32, H, C, xv, g, Upk, Wx, Hn, Cn, part, 4};
   std::vector<Variant> vs = {
       {"NW4 (production)        ", launch_v<4, 0>},
-      {"NW4 buffer-load H       ", launch_v<4, 0, true>},
-      {"LDS-DMA ring BK16 x3    ", launch_dma<0>},
+      {"LDS-DMA ring, generic   ", launch_dma<0, false>},
+      {"LDS-DMA ring, K16 (prod)", launch_dma<0>},
       {"DIAG: DMA + stamps      ", launch_dma<4>},
       {"DIAG: stamps, no stores ", launch_dma<5>},
       {"DIAG: DMA, no epilogue  ", launch_dma<1>},
