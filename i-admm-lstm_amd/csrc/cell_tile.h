@@ -361,7 +361,9 @@ IADMM_DEV void mainloop_dma_k16(const float* __restrict__ Abase, const float* __
   constexpr int NPA = NA * 2;
   constexpr int APW = (NPA + 3) / 4;
   // acc is not zeroed with moves: chunk 0's first MFMA of each accumulator takes an inline-zero C
-  // operand instead (128 fewer VALU writes per tile; chunk 0 is peeled for that)
+  // operand instead (128/160 fewer VALU writes per tile; chunk 0 is peeled for that).  At NA = 5
+  // the peeled head copies spill a few fragment registers (scratch, outside the loop: the loop
+  // itself stays spill- and VALU-free).
 
   const int lane = tid & 63;
   const int nk = K / kBKd;

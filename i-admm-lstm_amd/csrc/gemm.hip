@@ -128,7 +128,9 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(int64_t M, int Ni, int 
 // panel run back to back on one XCD (panel reused from its L2).
 // A_PACKED: W given as iadmm_gemm_pack_a's [nit][ceil(K/32)][NA*32][32] tiles (each DMA piece one
 // contiguous KiB) instead of row-major [Ni][K] (16 rows x 64 B per piece).
-template <bool ACC, bool A_PACKED, int NA>
+// K16 (A_PACKED, K % 16 == 0): the VALU-free main loop (cell_tile.h mainloop_dma_k16), bitwise the
+// same products and order.
+template <bool ACC, bool A_PACKED, int NA, bool K16 = false>
 __global__ __launch_bounds__(256, 2) void gemm_nt_dma_kernel(int64_t M, int Ni, int K, const float* X,
                                                              const float* W, float* out) {
   extern __shared__ __attribute__((aligned(16))) float ring[];
@@ -142,7 +144,11 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_dma_kernel(int64_t M, int Ni, 
   const int i0 = it * TI;
   const int64_t r0 = rt * 256;
   floatx16 acc[NA][2];
-  if constexpr (A_PACKED) {
+  if constexpr (A_PACKED && K16) {
+    const int64_t nkc32 = (K + kBK - 1) / kBK;
+    mainloop_dma_k16<NA>(W + (int64_t)it * nkc32 * TI * kBK, X + r0 * K, M - r0, K, K, ring, acc, tid, wave, jl, hf,
+                         [] {});
+  } else if constexpr (A_PACKED) {
     const int64_t nkc32 = (K + kBK - 1) / kBK;
     mainloop_dma<true, NA>(W + (int64_t)it * nkc32 * TI * kBK, TI, kBK, X + r0 * K, M - r0, K, K, ring, acc, tid,
                            wave, jl, hf, [] {});
@@ -178,23 +184,29 @@ inline int gemm_nt_tile(int64_t Ni) {
   return w160 < w128 ? 160 : 128;
 }
 
+template <bool ACC, bool A_PACKED, int NA, bool K16>
+int launch_gemm_nt_dma_t(dim3 grid, int64_t M, int64_t Ni, int64_t K, const float* X, const float* W, float* out,
+                         hipStream_t s) {
+  constexpr int lds = dma_ring_floats<NA>() * 4;
+  IADMM_ALLOW_LDS((gemm_nt_dma_kernel<ACC, A_PACKED, NA, K16>), lds);
+  hipLaunchKernelGGL((gemm_nt_dma_kernel<ACC, A_PACKED, NA, K16>), grid, dim3(256), lds, s, M, (int)Ni, (int)K, X, W,
+                     out);
+  IADMM_CHECK_LAUNCH();
+  return 0;
+}
+
 template <bool ACC, bool A_PACKED>
 int launch_gemm_nt_dma(int64_t M, int64_t Ni, int64_t K, const float* X, const float* W, float* out, hipStream_t s) {
   const int ti = gemm_nt_tile(Ni);
   const int64_t nit = (Ni + ti - 1) / ti, nrt = (M + 255) / 256;
   if (nit * nrt > 0x7fffffffLL) return IADMM_E_SIZE;
   const dim3 grid((unsigned)(nit * nrt));
-  if (ti == 160) {
-    constexpr int lds = dma_ring_floats<5>() * 4;
-    IADMM_ALLOW_LDS((gemm_nt_dma_kernel<ACC, A_PACKED, 5>), lds);
-    hipLaunchKernelGGL((gemm_nt_dma_kernel<ACC, A_PACKED, 5>), grid, dim3(256), lds, s, M, (int)Ni, (int)K, X, W, out);
-  } else {
-    constexpr int lds = dma_ring_floats<4>() * 4;
-    IADMM_ALLOW_LDS((gemm_nt_dma_kernel<ACC, A_PACKED, 4>), lds);
-    hipLaunchKernelGGL((gemm_nt_dma_kernel<ACC, A_PACKED, 4>), grid, dim3(256), lds, s, M, (int)Ni, (int)K, X, W, out);
-  }
-  IADMM_CHECK_LAUNCH();
-  return 0;
+  const bool k16 = A_PACKED && K % kBKd == 0;
+  if (ti == 160)
+    return k16 ? launch_gemm_nt_dma_t<ACC, A_PACKED, 5, A_PACKED>(grid, M, Ni, K, X, W, out, s)
+               : launch_gemm_nt_dma_t<ACC, A_PACKED, 5, false>(grid, M, Ni, K, X, W, out, s);
+  return k16 ? launch_gemm_nt_dma_t<ACC, A_PACKED, 4, A_PACKED>(grid, M, Ni, K, X, W, out, s)
+             : launch_gemm_nt_dma_t<ACC, A_PACKED, 4, false>(grid, M, Ni, K, X, W, out, s);
 }
 
 // Wpk[((it * nkc32 + kc) * TI + row) * 32 + kk] = W[it*TI + row][kc*32 + kk]  (0 outside)

@@ -53,4 +53,6 @@ def test_lanes_timer_spans(batch):
     n, mean = tm.stats_ms("k:lstm_cell")
     assert n == 16
     busy = tm.busy_ms("k:lstm_cell")
-    assert 0 < busy <= n * mean * (1 + 1e-6)
+    # busy_ms works on ref-relative event times, stats_ms on direct span times: each may round
+    # differently at the events' microsecond resolution
+    assert 0 < busy <= n * mean + n * 2e-3

@@ -28,6 +28,6 @@ done
 rm -rf "$raw"
 timeout -k 10 700 python3 -u bench.py $C4 --outer_T 200 --steps 1 --warmup 0 --cpu-sample 0 --alt-f16x3 0 \
   --in-place-scaling > "$out/bench_config4.json" 2> "$out/bench_config4.err"
-timeout -k 10 400 python3 -u bench_stage2.py --batch 512 --num_var 5000 --num_ineq 2500 --num_eq 2500 \
+[ "${SKIP_STAGE2:-0}" = 1 ] || timeout -k 10 400 python3 -u bench_stage2.py --batch 512 --num_var 5000 --num_ineq 2500 --num_eq 2500 \
   --steps 1 --warmup 0 --cpu-sample 0 > "$out/stage2_config4.json" 2> "$out/stage2_config4.err"
 echo "config-4 profile done: $out"
