@@ -108,3 +108,32 @@ def test_generate_data_cli(tmp_path):
     r = dataset.read_qp(out, [0, 1, 2], "cpu")
     ref = data.make_qp_batch(8, 3, 2, 3, device="cpu")
     assert torch.equal(r["A0"], ref["A0"]) and torch.equal(r["zu"], ref["zu"])
+
+
+def test_threaded_equals_sequential(tmp_path):
+    """The thread-pool reader/writer (workers > 1) produce exactly the sequential result."""
+    n, mi, me = 24, 7, 5
+    d = data.make_qp_batch(n, mi, me, 9, first_index=0, device="cpu")
+    seq, par = os.path.join(str(tmp_path), "seq"), os.path.join(str(tmp_path), "par")
+    dataset.write_qp(seq, d, mi, workers=1)
+    dataset.write_qp(par, d, mi, workers=4)
+    ids = [8, 0, 3, 5, 1]
+    a = dataset.read_qp(seq, ids, "cpu", workers=1)
+    b = dataset.read_qp(par, ids, "cpu", workers=4)
+    assert a.keys() == b.keys()
+    for k in a:
+        assert torch.equal(a[k], b[k]), k
+    for k in ("Q", "p", "A0", "zl", "zu"):
+        assert torch.equal(a[k], d[k][ids]), k
+
+
+def test_inconsistent_shapes_raise(tmp_path):
+    n, mi, me = 8, 3, 2
+    _reference_style_files(str(tmp_path), n, mi, me, 2)
+    with gzip.open(os.path.join(str(tmp_path), "qp_1.gz"), "rb") as f:
+        rec = pickle.load(f)  # file written by this test
+    rec["A0"] = rec["A0"][:, :-1]
+    with gzip.open(os.path.join(str(tmp_path), "qp_1.gz"), "wb") as f:
+        pickle.dump(rec, f)
+    with pytest.raises(ValueError):
+        dataset.read_qp(str(tmp_path), [0, 1], "cpu")
