@@ -727,39 +727,39 @@ template <int DIAG = 0>
 IADMM_DEV void cell_epi_compute_buf(floatx16 (&acc)[4][2], const float* sWp, int hf, CellEpiBuf& e) {
 #pragma unroll
   for (int r = 0; r < 2; ++r) {
-    const float2v in0 = splat2(e.in0[r]), in1 = splat2(e.in1[r]);
     float2v gs = splat2(0.f);
 #pragma unroll
     for (int qq = 0; qq < 4; ++qq) {
       __builtin_amdgcn_sched_barrier(0);  // one (rows, 4 units) group at a time: bounded live range
       const int jj0 = 8 * qq + 4 * hf;
       const float4 cold = e.cold[r][qq];
-      float4 cnew, hnew;
+      // both unit pairs of the group at once (float4v: two independent packed halves)
+      const float4* wp0 = reinterpret_cast<const float4*>(sWp + (jj0 >> 1) * 32);
+      const float4* wp1 = wp0 + 8;  // next pair's 128-B row
+      float4 w0[7], w1[7];
 #pragma unroll
-      for (int pp = 0; pp < 2; ++pp) {
-        const float4* wp = reinterpret_cast<const float4*>(sWp + ((jj0 >> 1) + pp) * 32);
-        float4 w4[7];
+      for (int i = 0; i < 7; ++i) { w0[i] = wp0[i]; w1[i] = wp1[i]; }
+      auto fld4 = [&](int f) -> float4v {
+        const float4& t0 = w0[f >> 1];
+        const float4& t1 = w1[f >> 1];
+        return (f & 1) ? float4v{t0.z, t0.w, t1.z, t1.w} : float4v{t0.x, t0.y, t1.x, t1.y};
+      };
+      const int q = qq * 4;
+      const float4v in0v = splat4(e.in0[r]), in1v = splat4(e.in1[r]);
+      float4v pre[4];
 #pragma unroll
-        for (int i = 0; i < 7; ++i) w4[i] = wp[i];
-        auto fld = [&](int f) -> float2v {
-          const float4& t = w4[f >> 1];
-          return (f & 1) ? float2v{t.z, t.w} : float2v{t.x, t.y};
-        };
-        const int q = qq * 4 + 2 * pp;
-        float2v pre[4];
-#pragma unroll
-        for (int g = 0; g < 4; ++g)
-          pre[g] = cell_pre2(in0, in1, float2v{acc[g][r][q], acc[g][r][q + 1]}, fld(3 * g), fld(3 * g + 1),
-                             fld(3 * g + 2));
-        const float2v ig = sigmoid_cell2(pre[0]), fg = sigmoid_cell2(pre[1]), og = sigmoid_cell2(pre[2]);
-        const float2v ug = tanh_cell2(pre[3]);
-        const float2v cv = pp ? float2v{cold.z, cold.w} : float2v{cold.x, cold.y};
-        const float2v c2 = ig * ug + fg * cv;
-        const float2v h2 = og * tanh_cell2(c2);
-        gs = fma2(h2, fld(12), gs);
-        if (pp == 0) { cnew.x = c2.x; cnew.y = c2.y; hnew.x = h2.x; hnew.y = h2.y; }
-        else         { cnew.z = c2.x; cnew.w = c2.y; hnew.z = h2.x; hnew.w = h2.y; }
-      }
+      for (int g = 0; g < 4; ++g)
+        pre[g] = cell_pre4(in0v, in1v, float4v{acc[g][r][q], acc[g][r][q + 1], acc[g][r][q + 2], acc[g][r][q + 3]},
+                           fld4(3 * g), fld4(3 * g + 1), fld4(3 * g + 2));
+      const float4v ig = sigmoid_cell4(pre[0]), fg = sigmoid_cell4(pre[1]), og = sigmoid_cell4(pre[2]);
+      const float4v ug = tanh_cell4(pre[3]);
+      const float4v cv = float4v{cold.x, cold.y, cold.z, cold.w};
+      const float4v c4 = ig * ug + fg * cv;
+      const float4v h4 = og * tanh_cell4(c4);
+      const float4v wh = fld4(12);
+      gs = fma2(float2v{h4.x, h4.y}, float2v{wh.x, wh.y}, gs);
+      gs = fma2(float2v{h4.z, h4.w}, float2v{wh.z, wh.w}, gs);
+      const float4 cnew = make_float4(c4.x, c4.y, c4.z, c4.w), hnew = make_float4(h4.x, h4.y, h4.z, h4.w);
       if (DIAG == 2) {  // timing diagnostic: no H'/C' stores (keep the values alive)
         gs.x += cnew.x + cnew.y + cnew.z + cnew.w;
       } else {

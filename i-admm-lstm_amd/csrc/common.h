@@ -95,6 +95,39 @@ IADMM_DEV float2v tanh_cell2(float2v x) {
   q = fma2(s, q, splat2(1.0f));
   return (x * p) * rcp2(q);
 }
+// Four-lane forms (two unit pairs at once): every operation splits into two independent packed
+// halves, so dependent packed ops never sit back to back (no s_nop hazard padding) and the
+// transcendentals come four at a time.  Same operation sequence: bitwise equal to the scalar forms.
+typedef float float4v __attribute__((ext_vector_type(4)));
+IADMM_DEV float4v splat4(float v) { return float4v{v, v, v, v}; }
+IADMM_DEV float4v fma4(float4v a, float4v b, float4v c) { return __builtin_elementwise_fma(a, b, c); }
+IADMM_DEV float4v exp2_4(float4v y) {
+  return float4v{__builtin_amdgcn_exp2f(y.x), __builtin_amdgcn_exp2f(y.y), __builtin_amdgcn_exp2f(y.z),
+                 __builtin_amdgcn_exp2f(y.w)};
+}
+IADMM_DEV float4v rcp4(float4v d) {
+  return float4v{__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y), __builtin_amdgcn_rcpf(d.z),
+                 __builtin_amdgcn_rcpf(d.w)};
+}
+IADMM_DEV float4v sigmoid_cell4(float4v x) { return rcp4(splat4(1.0f) + exp2_4(x * splat4(kNL2E))); }
+IADMM_DEV float4v tanh_cell4(float4v x) {
+  x = float4v{__builtin_amdgcn_fmed3f(x.x, -kTanhClamp, kTanhClamp), __builtin_amdgcn_fmed3f(x.y, -kTanhClamp, kTanhClamp),
+              __builtin_amdgcn_fmed3f(x.z, -kTanhClamp, kTanhClamp), __builtin_amdgcn_fmed3f(x.w, -kTanhClamp, kTanhClamp)};
+  const float4v s = x * x;
+  float4v p = fma4(s, splat4(kTp6), splat4(kTp5));
+  p = fma4(s, p, splat4(kTp4));
+  p = fma4(s, p, splat4(kTp3));
+  p = fma4(s, p, splat4(kTp2));
+  p = fma4(s, p, splat4(kTp1));
+  p = fma4(s, p, splat4(1.0f));
+  float4v q = fma4(s, splat4(kTq3), splat4(kTq2));
+  q = fma4(s, q, splat4(kTq1));
+  q = fma4(s, q, splat4(1.0f));
+  return (x * p) * rcp4(q);
+}
+IADMM_DEV float4v cell_pre4(float4v in0, float4v in1, float4v acc, float4v w0, float4v w1, float4v b) {
+  return fma4(in1, w1, fma4(in0, w0, b)) + acc;
+}
 IADMM_DEV float2v cell_pre2(float2v in0, float2v in1, float2v acc, float2v w0, float2v w1, float2v b) {
   return fma2(in1, w1, fma2(in0, w0, b)) + acc;
 }
