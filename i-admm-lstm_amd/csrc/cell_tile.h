@@ -816,12 +816,13 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void cell_fwd_kernel(Cell
 // H'/C' stores; 3 = epilogue without the C / xv / g loads.
 // DIAG 4: as 0, plus s_memtime stamps (kernel start, main loop end, epilogue operands landed,
 // epilogue end) of wave 0 of every workgroup into a.part[njt * M ...]; 5: same without the H'/C'
-// stores -- diagnostic builds only (tools/cellbench).
+// stores; 6: as 4 plus HW_ID / XCC_ID (8 words per workgroup: co-residency phase study) --
+// diagnostic builds only (tools/cellbench).
 template <int DIAG = 0, bool K16 = false>
 __global__ __launch_bounds__(256, 2) void cell_fwd_dma_kernel(CellArgsT a) {
   extern __shared__ __attribute__((aligned(16))) float dsm[];
   uint64_t t_start = 0, t_ml = 0;
-  if constexpr (DIAG == 4) t_start = __builtin_amdgcn_s_memtime();
+  if constexpr (DIAG == 4 || DIAG == 6) t_start = __builtin_amdgcn_s_memtime();
   float* ring = dsm;
   float* sW = dsm + kRingFloats;
   int jt, rt;
@@ -871,12 +872,17 @@ __global__ __launch_bounds__(256, 2) void cell_fwd_dma_kernel(CellArgsT a) {
     vm_wait<0>();  // the prefetched epilogue operands
     t_c = __builtin_amdgcn_s_memtime();
   }
-  cell_epi_compute_buf<DIAG == 4 ? 0 : (DIAG == 5 ? 2 : DIAG)>(acc, sW, hf, ei);
+  cell_epi_compute_buf<(DIAG == 4 || DIAG == 6) ? 0 : (DIAG == 5 ? 2 : DIAG)>(acc, sW, hf, ei);
   if constexpr (DIAG >= 4) {
     const uint64_t t_end = __builtin_amdgcn_s_memtime();
     if (tid == 0) {
-      uint64_t* st = reinterpret_cast<uint64_t*>(a.part + (int64_t)a.njt * a.M) + (int64_t)blockIdx.x * 4;
+      constexpr int W = DIAG == 6 ? 8 : 4;
+      uint64_t* st = reinterpret_cast<uint64_t*>(a.part + (int64_t)a.njt * a.M) + (int64_t)blockIdx.x * W;
       st[0] = t_start; st[1] = t_ml; st[2] = t_c; st[3] = t_end;
+      if constexpr (DIAG == 6) {
+        st[4] = __builtin_amdgcn_s_getreg((31 << 11) | 4);   // HW_REG_HW_ID
+        st[5] = __builtin_amdgcn_s_getreg((31 << 11) | 20);  // HW_REG_XCC_ID
+      }
     }
   }
 }

@@ -109,7 +109,7 @@ int main(int argc, char** argv) {
   const int njt = (h + 31) / 32, nkc32 = (h + 31) / 32;
   float *H, *C, *xv, *g, *Upk, *Wx, *Hn, *Cn, *part;
   CK(hipMalloc(&H, M * h * 4)); CK(hipMalloc(&C, M * h * 4)); CK(hipMalloc(&Hn, M * h * 4)); CK(hipMalloc(&Cn, M * h * 4));
-  CK(hipMalloc(&xv, M * 4)); CK(hipMalloc(&g, M * 4)); CK(hipMalloc(&part, (int64_t)njt * M * 4 + (int64_t)njt * ((M + 255) / 256) * 32));
+  CK(hipMalloc(&xv, M * 4)); CK(hipMalloc(&g, M * 4)); CK(hipMalloc(&part, (int64_t)njt * M * 4 + (int64_t)njt * ((M + 255) / 256) * 64));
   const int64_t nup = (int64_t)njt * nkc32 * 128 * 32, nwx = (int64_t)njt * 32 * 16;
   CK(hipMalloc(&Upk, nup * 4)); CK(hipMalloc(&Wx, nwx * 4));
   hipLaunchKernelGGL(fill, dim3(4096), dim3(256), 0, 0, H, M * h, 1u, 0.9f);
@@ -120,6 +120,21 @@ int main(int argc, char** argv) {
   hipLaunchKernelGGL(fill, dim3(256), dim3(256), 0, 0, Wx, nwx, 6u, 0.02f);
   CK(hipDeviceSynchronize());
   CellArgsT a{M, (int)h, njt, nkc32, H, C, xv, g, Upk, Wx, Hn, Cn, part, 4};
+  if (argc > 3 && std::string(argv[3]) == "phase") {  // raw DIAG-6 stamps -> argv[4] (tools/cellphase.py)
+    const int64_t nwg = njt * ((M + 255) / 256);
+    launch_dma<0>(a, M, 0);
+    launch_dma<6>(a, M, 0);
+    CK(hipDeviceSynchronize());
+    launch_dma<6>(a, M, 0);
+    CK(hipDeviceSynchronize());
+    std::vector<uint64_t> st(nwg * 8);
+    CK(hipMemcpy(st.data(), reinterpret_cast<char*>(part) + (int64_t)njt * M * 4, nwg * 64, hipMemcpyDeviceToHost));
+    FILE* f = fopen(argc > 4 ? argv[4] : "phase.bin", "wb");
+    fwrite(st.data(), 8, st.size(), f);
+    fclose(f);
+    printf("wrote %lld workgroups x 8 words\n", (long long)nwg);
+    return 0;
+  }
   std::vector<Variant> vs = {
       {"NW4 (production)        ", launch_v<4, 0>},
       {"LDS-DMA ring, generic   ", launch_dma<0, false>},
