@@ -43,7 +43,10 @@ def rel(a, b):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("M,h", [(700, 48), (257, 40), (64, 8), (300, 36), (513, 13), (100, 30), (1000, 800)])
+# h % 16 == 0 runs the VALU-free K16 loop: h = 16 (one chunk), 48 / 800 / 80 / 112 (head paths
+# (h/16 - 1) % 3 = 2 / 1 / 1 / 0) and partial hidden tiles (h % 32 = 16: the buffer epilogue's tail)
+@pytest.mark.parametrize("M,h", [(700, 48), (257, 40), (64, 8), (300, 36), (513, 13), (100, 30), (1000, 800),
+                                 (700, 16), (513, 64), (300, 112), (257, 80)])
 def test_cell_matches_fp64(M, h):
     if not torch.cuda.is_available():
         pytest.skip("no GPU")

@@ -82,7 +82,11 @@ def test_loss_grad_matches_autograd():
         assert rel_l2(mine.grad, ref.grad) < 1e-5
 
 
-@pytest.mark.parametrize("M,Ni,K", [(300, 40, 160), (1000, 130, 96), (257, 3, 50), (64, 800, 3200), (513, 136, 100)])
+# K % 16 == 0 with a packed A runs cell_tile.h mainloop_dma_k16: its three head paths ((K/16 - 1) % 3
+# = 0, 1, 2), the single-chunk case (K = 16) and both tile heights (NA = 4: 128 rows, 5: 160 rows)
+# are checked bitwise against the generic loop below
+@pytest.mark.parametrize("M,Ni,K", [(300, 40, 160), (1000, 130, 96), (257, 3, 50), (64, 800, 3200), (513, 136, 100),
+                                    (300, 160, 48), (200, 320, 16), (129, 64, 64)])
 def test_gemm_nt_matches_fp64(M, Ni, K):
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
