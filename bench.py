@@ -250,7 +250,7 @@ def main():
     world, rank, local = parallel.env()
     local, backend = parallel.device_and_backend(local)
     torch.cuda.set_device(local)
-    dist = parallel.init(backend, local) if world > 1 else None
+    dist = parallel.init(backend, local) if parallel.want_dist(world) else None
 
     n, mi, me, h, T, B = args.num_var, args.num_ineq, args.num_eq, args.hidden_dim, args.outer_T, args.batch
     N = n + mi + me
@@ -369,6 +369,7 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
+            "dist_backend": dist.get_backend() if dist else None,
             "dtype": "f32",
             "data": f"synthetic (generate_data.py:67-76 distribution, per-instance seeds); weights {weights_tag}",
             "config": {"workload": f"QP n={n} ineq={mi} eq={me} K={T} hidden={h} --test --scaling, "

@@ -37,7 +37,7 @@ def main():
     world, rank, local = parallel.env()
     local, backend = parallel.device_and_backend(local)
     torch.cuda.set_device(local)
-    dist = parallel.init(backend, local) if world > 1 else None
+    dist = parallel.init(backend, local) if parallel.want_dist(world) else None
     n, mi, me, h, T, B = args.num_var, args.num_ineq, args.num_eq, args.hidden_dim, args.outer_T, args.batch
     first, count = parallel.shard(world * B, world, rank)
     d = data.make_qp_batch(n, mi, me, count, first_index=first, device="cuda")
@@ -72,6 +72,8 @@ def main():
                           "n_gpus": world, "batch_per_gpu": B, "micro_batch": args.micro_batch, "outer_T": T,
                           "hidden_dim": h, "loss": loss,
                           "cell_gemm_tflops_equiv": 4 * fwd_flop * args.steps / el / 1e12,
+                          "dist_backend": dist.get_backend() if dist else None,
+                          "allreduce_calls": train.ALLREDUCE_CALLS,
                           "note": "cell GEMM work per step = forward + recompute + dH + dU = 4x forward flops"}))
     if dist:
         dist.destroy_process_group()

@@ -32,6 +32,15 @@ def device_and_backend(local_rank):
     return int(local_rank), "nccl"
 
 
+FORCE_DIST_ENV = "IADMM_FORCE_DIST"
+
+
+def want_dist(world):
+    """Initialise a process group: always for world > 1; at world 1 only with IADMM_FORCE_DIST=1
+    (exercises the RCCL branch and the gradient all-reduce on a one-GPU box)."""
+    return world > 1 or os.environ.get(FORCE_DIST_ENV) == "1"
+
+
 def shard(global_batch, world, rank):
     """Contiguous [start, start+count) of ``global_batch`` instances for ``rank`` (sizes differ by
     at most one when the batch does not divide)."""

@@ -19,11 +19,19 @@ def flat_grads(params):
     return torch.cat([p.grad.reshape(-1) if p.grad is not None else torch.zeros_like(p).reshape(-1) for p in params])
 
 
+ALLREDUCE_CALLS = 0  # gradient buckets all-reduced by this process (bench_train.py reports it)
+
+
 def allreduce_grads(params, dist, bucket_bytes=32 << 20):
     """Sum every parameter gradient over ranks: gradients are packed into contiguous buckets of
     at most ``bucket_bytes`` (one bucket at the reference's parameter count), all-reduced, and
-    copied back (fixed order, so every rank ends with bitwise identical gradients)."""
-    if dist is None or not dist.is_initialized() or dist.get_world_size() == 1:
+    copied back (fixed order, so every rank ends with bitwise identical gradients).  A world-1
+    group runs the collective too when IADMM_FORCE_DIST=1 (parallel.want_dist)."""
+    global ALLREDUCE_CALLS
+    from . import parallel
+    if dist is None or not dist.is_initialized():
+        return
+    if dist.get_world_size() == 1 and not parallel.want_dist(1):
         return
     params = [p for p in params if p.requires_grad]
     for p in params:
@@ -42,6 +50,7 @@ def allreduce_grads(params, dist, bucket_bytes=32 << 20):
     for bucket in buckets:
         flat = torch.cat([q.grad.reshape(-1) for q in bucket])
         dist.all_reduce(flat)
+        ALLREDUCE_CALLS += 1
         off = 0
         for q in bucket:
             q.grad.copy_(flat[off:off + q.numel()].view_as(q.grad))

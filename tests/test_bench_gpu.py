@@ -23,10 +23,14 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _run(args, nproc=1, timeout=600, shared=True):
+def _run(args, nproc=1, timeout=600, shared=True, extra_env=None, launcher=False):
+    """Run a bench script; under torch.distributed.run when nproc > 1 (or launcher=True), with the
+    ranks sharing cuda:0 over gloo when ``shared``, one GPU per rank over RCCL otherwise."""
     env = dict(os.environ)
+    env.update(extra_env or {})
     if nproc > 1 and shared:
         env["IADMM_SHARED_GPU"] = "1"
+    if nproc > 1 or launcher:
         cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
                "--master-addr", "127.0.0.1", "--master-port", str(_free_port())] + args
     else:
@@ -99,3 +103,21 @@ def test_bench_train_two_ranks_rccl():
               "--num_var", "32", "--num_ineq", "16", "--num_eq", "16", "--hidden_dim", "32", "--outer_T", "2"],
              nproc=2, shared=False)
     assert r["n_gpus"] == 2 and r["value"] > 0 and r["loss"] == r["loss"]
+
+
+def test_bench_rccl_world1():
+    """The RCCL branch of parallel.init on hardware with the one GPU a builder box has: a world-1
+    process group over nccl (IADMM_FORCE_DIST=1), barriers through RCCL."""
+    r = _run(["bench.py", "--batch", "4", "--steps", "1", "--warmup", "0", "--cpu-sample", "0"] + SMALL, nproc=1,
+             shared=False, extra_env={"IADMM_FORCE_DIST": "1"}, launcher=True)
+    assert r["n_gpus"] == 1 and r["value"] > 0 and r["dist_backend"] == "nccl"
+
+
+def test_bench_train_rccl_world1():
+    """Config 5's bucketed gradient all-reduce through RCCL (world 1: the collective runs, the
+    values are unchanged)."""
+    r = _run(["bench_train.py", "--batch", "2", "--micro_batch", "1", "--steps", "1", "--warmup", "0",
+              "--num_var", "32", "--num_ineq", "16", "--num_eq", "16", "--hidden_dim", "32", "--outer_T", "2"],
+             nproc=1, shared=False, extra_env={"IADMM_FORCE_DIST": "1"}, launcher=True)
+    assert r["n_gpus"] == 1 and r["value"] > 0 and r["loss"] == r["loss"] and r["dist_backend"] == "nccl"
+    assert r["allreduce_calls"] >= 1
