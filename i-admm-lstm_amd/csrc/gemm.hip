@@ -368,7 +368,12 @@ IADMM_DEV void gemm_tn_dma_body(int64_t M, int Ni, int No, int64_t rows_per_spli
 #pragma unroll
     for (int c = 0; c < 2; ++c) bv[c] = sy[kk * 256 + wave * 64 + c * 32 + jl];
   };
+  // A wave whose 64 output columns all lie past No (the last o tile when No % 256 != 0, e.g. the
+  // half-empty 13th tile of No = 4h = 3200) skips its MFMAs: its SIMD's matrix pipe goes to the
+  // co-resident workgroup instead of multiplying zeros.
+  const bool wact = o0 + wave * 64 < No;
   auto mma = [&](const float (&av)[NA], const float (&bv)[2]) {
+    if (!wact) return;
 #pragma unroll
     for (int a = 0; a < NA; ++a)
 #pragma unroll
@@ -499,6 +504,50 @@ __global__ void slab_reduce_kernel(int64_t nelem, int nsplit, const float* slab,
   }
 }
 
+// The same sums, four adjacent elements per thread (16-B loads) and eight splits in flight per
+// thread (loads issued together, adds kept in split order: bitwise the same as slab_reduce_kernel).
+// nelem % 4 == 0, 16-B aligned slab and out.
+__global__ void slab_reduce4_kernel(int64_t nelem, int nsplit, const float* slab, float* out, int acc) {
+  const int64_t n4 = nelem / 4;
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < n4; e += (int64_t)gridDim.x * blockDim.x) {
+    const float4* p = reinterpret_cast<const float4*>(slab) + e;
+    float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+    int k = 0;
+    for (; k + 8 <= nsplit; k += 8) {
+      float4 v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = p[(int64_t)(k + u) * n4];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) { s.x += v[u].x; s.y += v[u].y; s.z += v[u].z; s.w += v[u].w; }
+    }
+    for (; k < nsplit; ++k) {
+      const float4 v = p[(int64_t)k * n4];
+      s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+    }
+    float4* o = reinterpret_cast<float4*>(out) + e;
+    if (acc) {
+      const float4 q = *o;
+      s = make_float4(q.x + s.x, q.y + s.y, q.z + s.z, q.w + s.w);
+    }
+    *o = s;
+  }
+}
+
+static int launch_slab_reduce(int64_t nelem, int64_t ns, const float* slab, float* out, int accumulate,
+                              hipStream_t s) {
+  if (nelem % 4 == 0 && aligned16(slab) && aligned16(out)) {
+    const int64_t blocks = (nelem / 4 + 255) / 256;
+    hipLaunchKernelGGL(slab_reduce4_kernel, dim3((unsigned)(blocks < 8192 ? blocks : 8192)), dim3(256), 0, s,
+                       nelem, (int)ns, slab, out, accumulate);
+  } else {
+    const int64_t blocks = (nelem + 255) / 256;
+    hipLaunchKernelGGL(slab_reduce_kernel, dim3((unsigned)(blocks < 4096 ? blocks : 4096)), dim3(256), 0, s,
+                       nelem, (int)ns, slab, out, accumulate);
+  }
+  IADMM_CHECK_LAUNCH();
+  return 0;
+}
+
 }  // namespace iadmm
 
 using namespace iadmm;
@@ -590,20 +639,11 @@ extern "C" int iadmm_gemm_tn(int64_t M, int64_t Ni, int64_t No, int64_t rows_per
     }
   }
   IADMM_CHECK_LAUNCH();
-  const int64_t nelem = Ni * No;
-  const int64_t blocks = (nelem + 255) / 256;
-  hipLaunchKernelGGL(slab_reduce_kernel, dim3((unsigned)(blocks < 4096 ? blocks : 4096)), dim3(256), 0, s,
-                     nelem, (int)ns, slab, out, accumulate);
-  IADMM_CHECK_LAUNCH();
-  return 0;
+  return launch_slab_reduce(Ni * No, ns, slab, out, accumulate, s);
 }
 
 extern "C" int iadmm_slab_reduce(int64_t nelem, int64_t nsplit, const float* slab, float* out, int accumulate,
                                  void* stream) {
   if (nelem <= 0 || nsplit <= 0 || !slab || !out) return IADMM_E_ARG;
-  const int64_t blocks = (nelem + 255) / 256;
-  hipLaunchKernelGGL(slab_reduce_kernel, dim3((unsigned)(blocks < 4096 ? blocks : 4096)), dim3(256), 0,
-                     (hipStream_t)stream, nelem, (int)nsplit, slab, out, accumulate);
-  IADMM_CHECK_LAUNCH();
-  return 0;
+  return launch_slab_reduce(nelem, nsplit, slab, out, accumulate, (hipStream_t)stream);
 }
