@@ -156,30 +156,44 @@ __global__ __launch_bounds__(256, 2) void lstm_cell_bwd_kernel(CellBwdArgs a) {
   for (int q = 0; q < 16; ++q) whp[q] = 0.f;
   if constexpr (VEC) {
     // Packed epilogue: unit pairs through v_pk_*_f32 (the forward's gate values bit for bit:
-    // same operations as cell_epi_compute).  h % 4 == 0: a lane's 4 units are all valid or not.
+    // same operations as cell_epi_compute_buf).  h % 4 == 0: a lane's 4 units are all valid or not.
+    // Global accesses through buffer descriptors based at the workgroup's row panel, ranges ending
+    // at its last valid row (rows past M read 0 / are dropped; a NULL dH' / dC' is an empty
+    // descriptor reading 0): 32-bit lane offsets and immediates instead of 64-bit address VALU and
+    // load-then-select (the forward epilogue's treatment, cell_tile.h CellEpiBuf).
+    const int nvalid = (int)((M - rbase) < kRows ? (M - rbase) : kRows);
+    const int64_t pan = rbase * h;
+    auto rs = [](const float* base, int bytes) {
+      return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base), 0, bytes, 0x00020000);
+    };
+    const int pbytes = nvalid * h * 4;
+    const __amdgpu_buffer_rsrc_t rC = rs(a.C + pan, pbytes), rdH = rs(a.dHn ? a.dHn + pan : a.C, a.dHn ? pbytes : 0),
+                                 rdCn = rs(a.dCn ? a.dCn + pan : a.C, a.dCn ? pbytes : 0), rdC = rs(a.dC + pan, pbytes),
+                                 rdP = rs(a.dP + pan * 4, nvalid * 4 * h * 4), rxv = rs(a.xv + rbase, nvalid * 4),
+                                 rg = rs(a.g + rbase, nvalid * 4), rdq = rs(a.dq + rbase, nvalid * 4),
+                                 rin = rs(a.inpart + ((int64_t)jt * M + rbase) * 2, nvalid * 8);
+    const bool full = (jt + 1) * kJT <= h;
 #pragma unroll
     for (int r = 0; r < 2; ++r) {
-      const int64_t R = rbase + wave * 64 + r * 32 + jl;
-      const bool rok = R < M;
-      const float2v in0 = splat2(rok ? a.xv[R] : 0.f), in1 = splat2(rok ? a.g[R] : 0.f);
-      const float2v dqv = splat2(rok ? a.dq[R] : 0.f);
+      const int row = wave * 64 + r * 32 + jl;
+      const bool rok = row < nvalid;
+      const unsigned vr = (unsigned)row * 4u;
+      const unsigned vo = ((unsigned)row * (unsigned)h + (unsigned)(jt * kJT + 4 * hf)) * 4u;
+      const unsigned vp = ((unsigned)row * (unsigned)(4 * h) + (unsigned)(jt * kJT + 4 * hf)) * 4u;
+      const float2v in0 = splat2(__uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rxv, vr, 0, 0)));
+      const float2v in1 = splat2(__uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rg, vr, 0, 0)));
+      const float2v dqv = splat2(__uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rdq, vr, 0, 0)));
       float2v din0 = splat2(0.f), din1 = splat2(0.f);
 #pragma unroll
       for (int qq = 0; qq < 4; ++qq) {
         __builtin_amdgcn_sched_barrier(0);
         const int jj0 = 8 * qq + 4 * hf;
-        const int j0 = jt * kJT + jj0;
-        const int64_t o0 = R * h + j0;
-        const bool ok4 = rok && j0 < h;
-        // unconditional loads from a valid address, then a select (a conditional load here became
-        // a flat load through a pointer select with a private zero copy)
-        auto ld4z = [&](const float* base, bool ok) -> float4 {
-          const float4 t = *reinterpret_cast<const float4*>(ok ? base + o0 : a.C);
-          return ok ? t : make_float4(0.f, 0.f, 0.f, 0.f);
-        };
-        const float4 cin4 = ld4z(a.C, ok4);
-        const float4 dh4 = ld4z(a.dHn, ok4 && a.dHn);
-        const float4 dc4 = ld4z(a.dCn, ok4 && a.dCn);
+        const bool uok = full || jt * kJT + jj0 < h;
+        const bool ok4 = rok && uok;
+        const unsigned qa = uok ? 32u * qq : 0x80000000u;
+        const float4 cin4 = u2f4(__builtin_amdgcn_raw_buffer_load_b128(rC, vo + qa, 0, 0));
+        const float4 dh4 = u2f4(__builtin_amdgcn_raw_buffer_load_b128(rdH, vo + qa, 0, 0));
+        const float4 dc4 = u2f4(__builtin_amdgcn_raw_buffer_load_b128(rdCn, vo + qa, 0, 0));
         float4 dC4, dP4[4];
 #pragma unroll
         for (int pp = 0; pp < 2; ++pp) {
@@ -230,20 +244,17 @@ __global__ __launch_bounds__(256, 2) void lstm_cell_bwd_kernel(CellBwdArgs a) {
             din1 += ((dPi * fld(1) + dPf * fld(4)) + dPo * fld(7)) + dPu * fld(10);
           }
         }
-        if (ok4) {
-          float* dp = a.dP + R * (int64_t)(4 * h) + j0;
-          *reinterpret_cast<float4*>(a.dC + o0) = dC4;
+        __builtin_amdgcn_raw_buffer_store_b128(f42u(dC4), rdC, vo + qa, 0, 0);
 #pragma unroll
-          for (int g = 0; g < 4; ++g) *reinterpret_cast<float4*>(dp + g * h) = dP4[g];
-        }
+        for (int g = 0; g < 4; ++g)
+          __builtin_amdgcn_raw_buffer_store_b128(f42u(dP4[g]), rdP, vp + (unsigned)(g * h * 4) + qa, 0, 0);
       }
       float d0 = din0.x + din0.y, d1 = din1.x + din1.y;
       d0 += __shfl_xor(d0, 32, 64);
       d1 += __shfl_xor(d1, 32, 64);
-      if (hf == 0 && rok) {
-        a.inpart[((int64_t)jt * M + R) * 2 + 0] = d0;
-        a.inpart[((int64_t)jt * M + R) * 2 + 1] = d1;
-      }
+      const unsigned vi = hf ? 0x80000000u : (unsigned)row * 8u;
+      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(d0), rin, vi, 0, 0);
+      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(d1), rin, vi + 4u, 0, 0);
     }
   } else {
 #pragma unroll
