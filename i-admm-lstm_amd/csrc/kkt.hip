@@ -146,7 +146,17 @@ struct KktSplitArgs {
   const float* scal;
   float *dots, *part, *r;                // workspace: [B][N], [B][nbq+nba][n], [B][N]
   float *g, *btild, *rhovec, *rout;
+  // pass-1 input vector [v1 ; v2] (rows of stride ld1 / ld2): xv for the residual gradient, dg
+  // for its backward, [x ; y] for the loss
+  const float *v1, *v2;
+  int ld1, ld2;
+  float* aux;                            // workspace [B][nchunk][2]: per-chunk partial sums
+  const float *rf, *cp, *cd;             // backward: saved forward residual; loss: coefficients
+  float *dxv, *dx, *dy, *dz, *ds_inst, *primal, *dual;
 };
+
+// What the two combine kernels compute (the two streaming passes are shared).
+enum SplitMode { kResgrad = 0, kKktBwd = 1, kLoss = 2 };
 
 // One block of kRB rows starting at row0 of an [R x n] matrix Mx: wave w sweeps its rows over
 // all column panels (DOT: dot_s[r] for the block's rows, accumulated across panels), COL: the
@@ -222,9 +232,8 @@ __global__ __launch_bounds__(256, IADMM_KKT_MINWG) void kkt_split_p1(KktSplitArg
   const size_t b = blockIdx.x / a.S;
   const int s = blockIdx.x % a.S;
   const int lo = (int)((int64_t)s * nblk / a.S), hi = (int)((int64_t)(s + 1) * nblk / a.S);
-  const float* xvb = a.xv + b * N;
   for (int i = tid; i < N; i += blockDim.x) {
-    if (i < n) xs[i] = xvb[i]; else vs[i - n] = xvb[i];
+    if (i < n) xs[i] = a.v1[b * a.ld1 + i]; else vs[i - n] = a.v2[b * a.ld2 + (i - n)];
   }
   __syncthreads();
   int fsel = 0;
@@ -257,33 +266,74 @@ IADMM_DEV float sum_partials(const float* __restrict__ pb, int nb, int n, int i)
   return red;
 }
 
-// Combine kernels: one thread per row of K (grid = B x ceil(N / 256)).
+// Combine kernels: one thread per row of K (grid = B x nchunk chunks of 256 rows).
+//   kResgrad  r = K xv - b~ (+ b~, rho_vec, r_out)
+//   kKktBwd   dr = K dg (r := dr) and the chunk's share of ds (d s through 1/rho)
+//   kLoss     e_d = Qx + p + A0^T y, e_p = A0 x - z (r := [e_d ; e_p]) and the chunk's share of
+//             ||e_d||^2, ||e_p||^2
+// The chunk partial sums (aux) are block_sum's fixed tree, added in chunk order by kkt_split_c2.
+template <int MODE>
 __global__ __launch_bounds__(256) void kkt_split_c1(KktSplitArgs a, int nchunk) {
+  __shared__ float red_s[4];
   const int n = a.n, m = a.m, N = n + m, nblk = a.nbq + a.nba;
   const size_t b = blockIdx.x / nchunk;
-  const int i = (blockIdx.x % nchunk) * 256 + threadIdx.x;
-  if (i >= N) return;
+  const int chunk = blockIdx.x % nchunk;
+  const int i = chunk * 256 + threadIdx.x;
+  if (MODE == kResgrad && i >= N) return;
   const float sigma = a.sigma;
   const float* db = a.dots + b * N;
+  float s0 = 0.f, s1 = 0.f;
   if (i < n) {
     const float red = sum_partials(a.part + b * nblk * n, a.nba, n, i);
-    const float xi = a.xv[b * N + i];
-    const float b1 = sigma * a.x[b * n + i] - a.p[b * n + i];
-    const float r1 = ((db[i] + sigma * xi) + red) - b1;
-    a.r[b * N + i] = r1;
-    if (a.btild) a.btild[b * N + i] = b1;
-    if (a.rout) a.rout[b * N + i] = r1;
-  } else {
+    if constexpr (MODE == kResgrad) {
+      const float xi = a.xv[b * N + i];
+      const float b1 = sigma * a.x[b * n + i] - a.p[b * n + i];
+      const float r1 = ((db[i] + sigma * xi) + red) - b1;
+      a.r[b * N + i] = r1;
+      if (a.btild) a.btild[b * N + i] = b1;
+      if (a.rout) a.rout[b * N + i] = r1;
+    } else if constexpr (MODE == kKktBwd) {
+      a.r[b * N + i] = (db[i] + sigma * a.v1[b * a.ld1 + i]) + red;       // dr1
+    } else {
+      const float e = (db[i] + a.p[b * n + i]) + red;                      // e_d
+      a.r[b * N + i] = e;
+      s0 = e * e;
+    }
+  } else if (i < N) {
     const int j = i - n;
     const bool ineq = j < a.num_ineq;
-    const float rho = a.scal[ineq ? IADMM_S_RHO_IN : IADMM_S_RHO_EQ];
-    const float irho = a.scal[ineq ? IADMM_S_IRHO_IN : IADMM_S_IRHO_EQ];
-    const float b2 = a.z[b * m + j] - irho * a.y[b * m + j];
-    const float r2 = (db[i] + (-irho) * a.xv[b * N + i]) - b2;
-    a.r[b * N + i] = r2;
-    if (a.btild) a.btild[b * N + i] = b2;
-    if (a.rout) a.rout[b * N + i] = r2;
-    if (a.rhovec) a.rhovec[b * m + j] = rho;
+    if constexpr (MODE == kResgrad) {
+      const float rho = a.scal[ineq ? IADMM_S_RHO_IN : IADMM_S_RHO_EQ];
+      const float irho = a.scal[ineq ? IADMM_S_IRHO_IN : IADMM_S_IRHO_EQ];
+      const float b2 = a.z[b * m + j] - irho * a.y[b * m + j];
+      const float r2 = (db[i] + (-irho) * a.xv[b * N + i]) - b2;
+      a.r[b * N + i] = r2;
+      if (a.btild) a.btild[b * N + i] = b2;
+      if (a.rout) a.rout[b * N + i] = r2;
+      if (a.rhovec) a.rhovec[b * m + j] = rho;
+    } else if constexpr (MODE == kKktBwd) {
+      // diota = -dg2 r2 + dr2 (y - v) ; ds += kappa * (-diota / rho^2)   (kappa: d rho / d s)
+      const float rho = a.scal[ineq ? IADMM_S_RHO_IN : IADMM_S_RHO_EQ];
+      const float irho = a.scal[ineq ? IADMM_S_IRHO_IN : IADMM_S_IRHO_EQ];
+      const float kappa = ineq ? 1.f : 1e3f;
+      const float dg2 = a.v2[b * a.ld2 + j];
+      const float dr2 = db[i] + (-irho) * dg2;
+      const float diota = -dg2 * a.rf[b * N + i] + dr2 * (a.y[b * m + j] - a.xv[b * N + i]);
+      s0 = kappa * (-diota / (rho * rho));
+      a.r[b * N + i] = dr2;
+    } else {
+      const float e = db[i] - a.z[b * m + j];                              // e_p
+      a.r[b * N + i] = e;
+      s1 = e * e;
+    }
+  }
+  if constexpr (MODE != kResgrad) {
+    s0 = block_sum(s0, red_s);
+    if constexpr (MODE == kLoss) s1 = block_sum(s1, red_s);
+    if (threadIdx.x == 0) {
+      a.aux[(b * nchunk + chunk) * 2 + 0] = s0;
+      a.aux[(b * nchunk + chunk) * 2 + 1] = s1;
+    }
   }
 }
 
@@ -318,16 +368,66 @@ __global__ __launch_bounds__(256, IADMM_KKT_MINWG) void kkt_split_p2(KktSplitArg
   }
 }
 
+//   kResgrad  g = [sum part + sigma r1 ; A0 r1 - r2 / rho]
+//   kKktBwd   dxv += K^T dr, dx -= sigma dr1, dz -= dr2, dy += dr2 / rho, ds_inst = sum of chunks
+//   kLoss     dx = cd Q^T e_d/|e_d| + cp A0^T e_p/|e_p|, dy = cd A0 e_d/|e_d|, dz = -cp e_p/|e_p|,
+//             primal = |e_p|, dual = |e_d|  (e/|e| := 0 when |e| = 0, like torch's norm backward)
+template <int MODE>
 __global__ __launch_bounds__(256) void kkt_split_c2(KktSplitArgs a, int nchunk) {
   const int n = a.n, m = a.m, N = n + m, nblk = a.nbq + a.nba;
   const size_t b = blockIdx.x / nchunk;
-  const int i = (blockIdx.x % nchunk) * 256 + threadIdx.x;
-  if (i >= N) return;
-  if (i < n) {
-    a.g[b * N + i] = sum_partials(a.part + b * nblk * n, nblk, n, i) + a.sigma * a.r[b * N + i];
+  const int chunk = blockIdx.x % nchunk;
+  const int i = chunk * 256 + threadIdx.x;
+  const float* pb = a.part + b * nblk * n;
+  const float* rb = a.r + b * N;
+  if constexpr (MODE == kResgrad) {
+    if (i >= N) return;
+    if (i < n) {
+      a.g[b * N + i] = sum_partials(pb, nblk, n, i) + a.sigma * rb[i];
+    } else {
+      const float irho = a.scal[(i - n) < a.num_ineq ? IADMM_S_IRHO_IN : IADMM_S_IRHO_EQ];
+      a.g[b * N + i] = a.dots[b * N + i] + (-irho) * rb[i];
+    }
+  } else if constexpr (MODE == kKktBwd) {
+    if (chunk == 0 && threadIdx.x == 0) {
+      float ds = 0.f;
+      for (int c = 0; c < nchunk; ++c) ds += a.aux[(b * nchunk + c) * 2];
+      a.ds_inst[b] = ds;
+    }
+    if (i >= N) return;
+    if (i < n) {
+      const float dr1 = rb[i];
+      a.dxv[b * N + i] += sum_partials(pb, nblk, n, i) + a.sigma * dr1;
+      a.dx[b * n + i] += -a.sigma * dr1;
+    } else {
+      const int j = i - n;
+      const float irho = a.scal[j < a.num_ineq ? IADMM_S_IRHO_IN : IADMM_S_IRHO_EQ];
+      const float dr2 = rb[i];
+      a.dxv[b * N + i] += a.dots[b * N + i] + (-irho) * dr2;
+      a.dz[b * m + j] += -dr2;
+      a.dy[b * m + j] += irho * dr2;
+    }
   } else {
-    const float irho = a.scal[(i - n) < a.num_ineq ? IADMM_S_IRHO_IN : IADMM_S_IRHO_EQ];
-    a.g[b * N + i] = a.dots[b * N + i] + (-irho) * a.r[b * N + i];
+    float dd = 0.f, pp = 0.f;
+    for (int c = 0; c < nchunk; ++c) {
+      dd += a.aux[(b * nchunk + c) * 2 + 0];
+      pp += a.aux[(b * nchunk + c) * 2 + 1];
+    }
+    const float nd = sqrtf(dd), np = sqrtf(pp);
+    if (chunk == 0 && threadIdx.x == 0) {
+      if (a.primal) a.primal[b] = np;
+      if (a.dual) a.dual[b] = nd;
+    }
+    if (i >= N) return;
+    const float cp = a.cp ? a.cp[b] : 0.f, cd = a.cd ? a.cd[b] : 0.f;
+    const float sd = nd > 0.f ? cd / nd : 0.f, sp = np > 0.f ? cp / np : 0.f;
+    if (i < n) {
+      if (a.dx) a.dx[b * n + i] = sd * sum_partials(pb, a.nbq, n, i) + sp * sum_partials(pb + (size_t)a.nbq * n, a.nba, n, i);
+    } else {
+      const int j = i - n;
+      if (a.dy) a.dy[b * m + j] = sd * a.dots[b * N + i];
+      if (a.dz) a.dz[b * m + j] = -sp * rb[i];
+    }
   }
 }
 
@@ -549,19 +649,25 @@ static int launch_split(dim3 grid, size_t lds, const KktSplitArgs& a, hipStream_
 }
 
 static int64_t kkt_split_blocks(int64_t n, int64_t m) { return (n + kRB - 1) / kRB + (m + kRB - 1) / kRB; }
+static int64_t kkt_split_chunks(int64_t n, int64_t m) { return (n + m + 255) / 256; }
 
 extern "C" int64_t iadmm_kkt_resgrad_ws_bytes(int64_t B, int64_t n, int64_t m) {
   if (B <= 0 || n <= 0 || m < 0) return 0;
-  return B * (2 * (n + m) + kkt_split_blocks(n, m) * n) * (int64_t)sizeof(float);
+  return B * (2 * (n + m) + kkt_split_blocks(n, m) * n + 2 * kkt_split_chunks(n, m)) * (int64_t)sizeof(float);
 }
 
-extern "C" int iadmm_kkt_resgrad(int64_t B, int64_t n, int64_t m, int64_t num_ineq,
-                                 const float* Q, const float* A0, const float* p, const float* x,
-                                 const float* y, const float* z, const float* xv, float sigma,
-                                 const float* scal, float* g, float* btild, float* rho_vec,
-                                 float* r_out, void* ws, int64_t ws_bytes, void* stream) {
-  if (B <= 0 || n <= 0 || m < 0 || num_ineq < 0 || num_ineq > m) return IADMM_E_ARG;
-  if (!Q || !p || !x || !xv || !scal || !g || (m > 0 && (!A0 || !y || !z))) return IADMM_E_ARG;
+template <int MODE>
+static int launch_combine(int pass, int64_t B, int nchunk, const KktSplitArgs& a, hipStream_t s) {
+  if (pass == 1) hipLaunchKernelGGL((kkt_split_c1<MODE>), dim3((unsigned)(B * nchunk)), dim3(256), 0, s, a, nchunk);
+  else hipLaunchKernelGGL((kkt_split_c2<MODE>), dim3((unsigned)(B * nchunk)), dim3(256), 0, s, a, nchunk);
+  IADMM_CHECK_LAUNCH();
+  return 0;
+}
+
+// The row-block split pipeline p1 -> c1 -> [p2] -> c2 for one of the three modes.  ``a`` carries
+// the mode's inputs/outputs; the geometry, workspace carving and pass-1 vector are filled here.
+static int run_split(int mode, int64_t B, int64_t n, int64_t m, KktSplitArgs a, void* ws, int64_t ws_bytes,
+                     bool pass2, hipStream_t s) {
   if (!ws || ws_bytes < iadmm_kkt_resgrad_ws_bytes(B, n, m) || !aligned16(ws)) return IADMM_E_ARG;
   const int64_t nbq = (n + kRB - 1) / kRB, nba = (m + kRB - 1) / kRB, nblk = nbq + nba;
   const int ng = ng_for(n < kPanelNG * 256 ? n : kPanelNG * 256);
@@ -577,30 +683,80 @@ extern "C" int iadmm_kkt_resgrad(int64_t B, int64_t n, int64_t m, int64_t num_in
   // the chip at its end -- and at most one workgroup per block
   int64_t S = IADMM_KKT_WG_TARGET / B;
   S = S < 1 ? 1 : (S > nblk ? nblk : S);
-  if (B * S > 0x7fffffff || B * ((n + m + 255) / 256) > 0x7fffffff) return IADMM_E_SIZE;
+  const int64_t nchunk = kkt_split_chunks(n, m);
+  if (B * S > 0x7fffffff || B * nchunk > 0x7fffffff) return IADMM_E_SIZE;
   float* w = static_cast<float*>(ws);
-  KktSplitArgs a{(int)n, (int)m, (int)num_ineq, (int)S, (int)nbq, (int)nba, dbuf ? 1 : 0, Q, A0, p, x, y, z, xv,
-                 sigma, scal, w, w + B * (n + m), w + B * (n + m) + B * nblk * n, g, btild, rho_vec, r_out};
-  const bool vec = (n % 4 == 0) && aligned16(Q) && (m == 0 || aligned16(A0));
-  hipStream_t s = (hipStream_t)stream;
-  const dim3 grid((unsigned)(B * S)), blk(256);
-  int rc = 0;
-  if (ng == 1) rc = vec ? launch_split<1, true>(grid, lds, a, s, 1) : launch_split<1, false>(grid, lds, a, s, 1);
-  else if (ng == 2) rc = vec ? launch_split<2, true>(grid, lds, a, s, 1) : launch_split<2, false>(grid, lds, a, s, 1);
-  else if (ng == 4) rc = vec ? launch_split<4, true>(grid, lds, a, s, 1) : launch_split<4, false>(grid, lds, a, s, 1);
-  else rc = vec ? launch_split<kPanelNG, true>(grid, lds, a, s, 1) : launch_split<kPanelNG, false>(grid, lds, a, s, 1);
-  if (rc) return rc;
-  const int nchunk = (int)((n + m + 255) / 256);
-  hipLaunchKernelGGL(kkt_split_c1, dim3((unsigned)(B * nchunk)), blk, 0, s, a, nchunk);
-  IADMM_CHECK_LAUNCH();
-  if (ng == 1) rc = vec ? launch_split<1, true>(grid, lds, a, s, 2) : launch_split<1, false>(grid, lds, a, s, 2);
-  else if (ng == 2) rc = vec ? launch_split<2, true>(grid, lds, a, s, 2) : launch_split<2, false>(grid, lds, a, s, 2);
-  else if (ng == 4) rc = vec ? launch_split<4, true>(grid, lds, a, s, 2) : launch_split<4, false>(grid, lds, a, s, 2);
-  else rc = vec ? launch_split<kPanelNG, true>(grid, lds, a, s, 2) : launch_split<kPanelNG, false>(grid, lds, a, s, 2);
-  if (rc) return rc;
-  hipLaunchKernelGGL(kkt_split_c2, dim3((unsigned)(B * nchunk)), blk, 0, s, a, nchunk);
-  IADMM_CHECK_LAUNCH();
-  return 0;
+  a.n = (int)n; a.m = (int)m; a.S = (int)S; a.nbq = (int)nbq; a.nba = (int)nba; a.dbuf = dbuf ? 1 : 0;
+  a.dots = w;
+  a.part = w + B * (n + m);
+  a.r = a.part + B * nblk * n;
+  a.aux = a.r + B * (n + m);
+  const bool vec = (n % 4 == 0) && aligned16(a.Q) && (m == 0 || aligned16(a.A0));
+  const dim3 grid((unsigned)(B * S));
+  auto stream_pass = [&](int pass) {
+    if (ng == 1) return vec ? launch_split<1, true>(grid, lds, a, s, pass) : launch_split<1, false>(grid, lds, a, s, pass);
+    if (ng == 2) return vec ? launch_split<2, true>(grid, lds, a, s, pass) : launch_split<2, false>(grid, lds, a, s, pass);
+    if (ng == 4) return vec ? launch_split<4, true>(grid, lds, a, s, pass) : launch_split<4, false>(grid, lds, a, s, pass);
+    return vec ? launch_split<kPanelNG, true>(grid, lds, a, s, pass) : launch_split<kPanelNG, false>(grid, lds, a, s, pass);
+  };
+  auto combine = [&](int pass) {
+    if (mode == kResgrad) return launch_combine<kResgrad>(pass, B, (int)nchunk, a, s);
+    if (mode == kKktBwd) return launch_combine<kKktBwd>(pass, B, (int)nchunk, a, s);
+    return launch_combine<kLoss>(pass, B, (int)nchunk, a, s);
+  };
+  int rc = stream_pass(1);
+  if (!rc) rc = combine(1);
+  if (!rc && pass2) rc = stream_pass(2);
+  if (!rc) rc = combine(2);
+  return rc;
+}
+
+extern "C" int iadmm_kkt_resgrad(int64_t B, int64_t n, int64_t m, int64_t num_ineq,
+                                 const float* Q, const float* A0, const float* p, const float* x,
+                                 const float* y, const float* z, const float* xv, float sigma,
+                                 const float* scal, float* g, float* btild, float* rho_vec,
+                                 float* r_out, void* ws, int64_t ws_bytes, void* stream) {
+  if (B <= 0 || n <= 0 || m < 0 || num_ineq < 0 || num_ineq > m) return IADMM_E_ARG;
+  if (!Q || !p || !x || !xv || !scal || !g || (m > 0 && (!A0 || !y || !z))) return IADMM_E_ARG;
+  KktSplitArgs a{};
+  a.num_ineq = (int)num_ineq;
+  a.Q = Q; a.A0 = A0; a.p = p; a.x = x; a.y = y; a.z = z; a.xv = xv;
+  a.sigma = sigma; a.scal = scal;
+  a.g = g; a.btild = btild; a.rhovec = rho_vec; a.rout = r_out;
+  a.v1 = xv; a.v2 = xv + n; a.ld1 = a.ld2 = (int)(n + m);
+  return run_split(kResgrad, B, n, m, a, ws, ws_bytes, true, (hipStream_t)stream);
+}
+
+extern "C" int iadmm_kkt_bwd_split(int64_t B, int64_t n, int64_t m, int64_t num_ineq, const float* Q,
+                                   const float* A0, const float* xv, const float* y, const float* r,
+                                   const float* dg, float sigma, const float* scal, float* dxv, float* dx,
+                                   float* dy, float* dz, float* ds_inst, void* ws, int64_t ws_bytes,
+                                   void* stream) {
+  if (B <= 0 || n <= 0 || m < 0 || num_ineq < 0 || num_ineq > m) return IADMM_E_ARG;
+  if (!Q || !xv || !r || !dg || !scal || !dxv || !dx || !ds_inst || (m > 0 && (!A0 || !y || !dy || !dz)))
+    return IADMM_E_ARG;
+  KktSplitArgs a{};
+  a.num_ineq = (int)num_ineq;
+  a.Q = Q; a.A0 = A0; a.y = y; a.xv = xv;
+  a.sigma = sigma; a.scal = scal;
+  a.v1 = dg; a.v2 = dg + n; a.ld1 = a.ld2 = (int)(n + m);
+  a.rf = r;
+  a.dxv = dxv; a.dx = dx; a.dy = dy; a.dz = dz; a.ds_inst = ds_inst;
+  return run_split(kKktBwd, B, n, m, a, ws, ws_bytes, true, (hipStream_t)stream);
+}
+
+extern "C" int iadmm_loss_grad_split(int64_t B, int64_t n, int64_t m, const float* Q, const float* p,
+                                     const float* A0, const float* x, const float* y, const float* z,
+                                     const float* cp, const float* cd, float* primal, float* dual, float* dx,
+                                     float* dy, float* dz, void* ws, int64_t ws_bytes, void* stream) {
+  if (B <= 0 || n <= 0 || m < 0 || !Q || !p || !x || (m > 0 && (!A0 || !y || !z))) return IADMM_E_ARG;
+  KktSplitArgs a{};
+  a.Q = Q; a.A0 = A0; a.p = p; a.z = z;
+  a.v1 = x; a.v2 = y; a.ld1 = (int)n; a.ld2 = (int)m;
+  a.cp = cp; a.cd = cd;
+  a.primal = primal; a.dual = dual; a.dx = dx; a.dy = dy; a.dz = dz;
+  // the second sweep only feeds the gradient; the norms come out of the first
+  return run_split(kLoss, B, n, m, a, ws, ws_bytes, dx || dy || dz, (hipStream_t)stream);
 }
 
 extern "C" int iadmm_kkt_lsres(int64_t B, int64_t n, int64_t m, int64_t num_ineq,

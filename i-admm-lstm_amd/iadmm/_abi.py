@@ -56,6 +56,9 @@ SIGNATURES = {
     "iadmm_kkt_bwd": (cint, [i64, i64, i64, i64, vp, vp, vp, vp, vp, vp, f32, vp, vp, vp, vp, vp, vp, vp]),
     "iadmm_sched_bwd": (cint, [vp, vp, i64, vp, i64, vp, i64, vp, vp, vp, vp]),
     "iadmm_loss_grad": (cint, [i64, i64, i64] + [vp] * 13 + [vp]),
+    "iadmm_kkt_bwd_split": (cint, [i64, i64, i64, i64, vp, vp, vp, vp, vp, vp, f32, vp, vp, vp, vp, vp, vp, vp, i64,
+                                   vp]),
+    "iadmm_loss_grad_split": (cint, [i64, i64, i64] + [vp] * 14 + [i64, vp]),
 }
 
 ERRORS = {-1: "bad argument", -2: "size beyond kernel limit", -3: "misaligned pointer"}

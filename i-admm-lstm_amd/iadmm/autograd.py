@@ -95,7 +95,9 @@ class LossFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, y, z, data):
         Q, pv, A0 = data
-        _, pr, du = ops.metrics(Q, pv, A0, x, y, z)   # one sweep; the gradient sweep runs in backward
+        # one sweep (row-block split: fills the chip at the micro-batch); the gradient sweep runs in
+        # backward
+        pr, du, _, _, _ = ops.loss_grad(Q, pv, A0, x, y, z, want_grad=False)
         ctx.save_for_backward(x, y, z)
         ctx.data = data
         return pr, du

@@ -354,12 +354,21 @@ def in_reduce(inpart, dxv, dg=None):
     return dg
 
 
-def kkt_bwd(Q, A0, xv, y, r, dg, sigma, scal, num_ineq, dxv, dx, dy, dz):
+def kkt_bwd(Q, A0, xv, y, r, dg, sigma, scal, num_ineq, dxv, dx, dy, dz, split=True, ws=None):
+    """Backward of :func:`kkt_resgrad` (accumulates into dxv, dx, dy, dz; returns ds per
+    instance).  ``split``: the row-block split (iadmm_kkt_bwd_split, fills the chip at the
+    training micro-batch); False: one workgroup per instance (iadmm_kkt_bwd)."""
     B, n = Q.shape[0], Q.shape[1]
     m = A0.shape[1]
     ds = empty(B, like=Q)
-    _abi.call("iadmm_kkt_bwd", B, n, m, int(num_ineq), _p(Q), _p(A0), _p(xv), _p(y), _p(r), _p(dg), float(sigma),
-              _p(scal), _p(dxv), _p(dx), _p(dy), _p(dz), _p(ds), _stream())
+    if split:
+        ws = kkt_resgrad_ws(B, n, m, Q.device) if ws is None else ws
+        _abi.call("iadmm_kkt_bwd_split", B, n, m, int(num_ineq), _p(Q), _p(A0), _p(xv), _p(y), _p(r), _p(dg),
+                  float(sigma), _p(scal), _p(dxv), _p(dx), _p(dy), _p(dz), _p(ds), _p(ws), ws.numel() * 4,
+                  _stream())
+    else:
+        _abi.call("iadmm_kkt_bwd", B, n, m, int(num_ineq), _p(Q), _p(A0), _p(xv), _p(y), _p(r), _p(dg),
+                  float(sigma), _p(scal), _p(dxv), _p(dx), _p(dy), _p(dz), _p(ds), _stream())
     return ds
 
 
@@ -368,14 +377,20 @@ def sched_bwd(rho_param, alpha_param, t, upd_partials, kkt_ds, drho, dalpha, dbh
               _p(kkt_ds), kkt_ds.shape[0], _p(drho), _p(dalpha), _p(dbh), _stream())
 
 
-def loss_grad(Q, p, A0, x, y, z, cp=None, cd=None, want_grad=True):
-    """(primal[B], dual[B], dx, dy, dz) of utils.py:68-71 with upstream coefficients cp, cd [B]."""
+def loss_grad(Q, p, A0, x, y, z, cp=None, cd=None, want_grad=True, split=True, ws=None):
+    """(primal[B], dual[B], dx, dy, dz) of utils.py:68-71 with upstream coefficients cp, cd [B].
+    ``split`` as for :func:`kkt_bwd` (iadmm_loss_grad_split / iadmm_loss_grad)."""
     B, n = Q.shape[0], Q.shape[1]
     m = A0.shape[1]
     pr, du = empty(B, like=Q), empty(B, like=Q)
     dx = dy = dz = None
     if want_grad:
         dx, dy, dz = empty(B, n, like=Q), empty(B, m, like=Q), empty(B, m, like=Q)
-    _abi.call("iadmm_loss_grad", B, n, m, _p(Q), _p(p), _p(A0), _p(x), _p(y), _p(z), _p(cp), _p(cd), _p(pr), _p(du),
-              _p(dx), _p(dy), _p(dz), _stream())
+    if split:
+        ws = kkt_resgrad_ws(B, n, m, Q.device) if ws is None else ws
+        _abi.call("iadmm_loss_grad_split", B, n, m, _p(Q), _p(p), _p(A0), _p(x), _p(y), _p(z), _p(cp), _p(cd),
+                  _p(pr), _p(du), _p(dx), _p(dy), _p(dz), _p(ws), ws.numel() * 4, _stream())
+    else:
+        _abi.call("iadmm_loss_grad", B, n, m, _p(Q), _p(p), _p(A0), _p(x), _p(y), _p(z), _p(cp), _p(cd), _p(pr),
+                  _p(du), _p(dx), _p(dy), _p(dz), _stream())
     return pr, du, dx, dy, dz

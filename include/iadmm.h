@@ -69,7 +69,8 @@ int iadmm_schedule_fixed_alpha(const float* scal_in, float alpha, float* scal_ou
  * The rows of Q and A0 are split into fixed 256-row blocks spread over enough workgroups to fill
  * the chip at any B; column sums are combined per block in block order, so g does not depend on
  * B (or on how a batch is sharded).  ws: caller-owned, 16-B aligned device workspace of at least
- * iadmm_kkt_resgrad_ws_bytes(B, n, m) bytes.  Limit: 2n + m floats of LDS <= 160 KiB. */
+ * iadmm_kkt_resgrad_ws_bytes(B, n, m) bytes (the same size serves iadmm_kkt_bwd_split and
+ * iadmm_loss_grad_split).  Limit: 2n + m floats of LDS <= 160 KiB. */
 int64_t iadmm_kkt_resgrad_ws_bytes(int64_t B, int64_t n, int64_t m);
 int iadmm_kkt_resgrad(int64_t B, int64_t n, int64_t m, int64_t num_ineq,
                       const float* Q, const float* A0, const float* p,
@@ -265,6 +266,16 @@ int iadmm_kkt_bwd(int64_t B, int64_t n, int64_t m, int64_t num_ineq, const float
                   float sigma, const float* scal, float* dxv, float* dx, float* dy, float* dz,
                   float* ds_inst, void* stream);
 
+/* iadmm_kkt_bwd on the row-block split of iadmm_kkt_resgrad (the same two streaming passes over
+ * Q and A0, spread over enough workgroups to fill the chip at any B, e.g. the training
+ * micro-batch of 128); same outputs, block-order summation (bitwise independent of B).
+ * ws: >= iadmm_kkt_resgrad_ws_bytes(B, n, m) bytes, 16-B aligned. */
+int iadmm_kkt_bwd_split(int64_t B, int64_t n, int64_t m, int64_t num_ineq, const float* Q,
+                        const float* A0, const float* xv, const float* y, const float* r,
+                        const float* dg, float sigma, const float* scal, float* dxv, float* dx,
+                        float* dy, float* dz, float* ds_inst, void* ws, int64_t ws_bytes,
+                        void* stream);
+
 /* drho[t] += s(1-s) sum(ds), dalpha[t] += 2 sig(alpha_t)(1-sig(alpha_t)) sum(da), dbh += sum(db). */
 int iadmm_sched_bwd(const float* rho_param, const float* alpha_param, int64_t t,
                     const float* upd_partials, int64_t nblk, const float* kkt_ds, int64_t B,
@@ -277,6 +288,13 @@ int iadmm_loss_grad(int64_t B, int64_t n, int64_t m, const float* Q, const float
                     const float* A0, const float* x, const float* y, const float* z,
                     const float* cp, const float* cd, float* primal, float* dual, float* dx,
                     float* dy, float* dz, void* stream);
+
+/* iadmm_loss_grad on the row-block split (see iadmm_kkt_bwd_split); with dx = dy = dz = NULL only
+ * the first streaming pass runs (primal/dual only).  ws as for iadmm_kkt_bwd_split. */
+int iadmm_loss_grad_split(int64_t B, int64_t n, int64_t m, const float* Q, const float* p,
+                          const float* A0, const float* x, const float* y, const float* z,
+                          const float* cp, const float* cd, float* primal, float* dual, float* dx,
+                          float* dy, float* dz, void* ws, int64_t ws_bytes, void* stream);
 
 #ifdef __cplusplus
 }

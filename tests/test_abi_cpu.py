@@ -40,9 +40,10 @@ def test_size_queries_without_gpu():
     assert lib.iadmm_lstm_ntiles(40) == 2
     assert lib.iadmm_lstm_packed_floats(800) == 25 * 25 * 128 * 32
     assert lib.iadmm_version() > 0
-    # KKT workspace: dots + r (2 (n+m)) and one partial column-sum vector per 256-row block
-    assert lib.iadmm_kkt_resgrad_ws_bytes(3, 1000, 1000) == 3 * (2 * 2000 + (4 + 4) * 1000) * 4
-    assert lib.iadmm_kkt_resgrad_ws_bytes(1, 24, 0) == (2 * 24 + 1 * 24) * 4
+    # KKT workspace: dots + r (2 (n+m)), one partial column-sum vector per 256-row block and two
+    # partial sums per 256-row chunk of [n ; m]
+    assert lib.iadmm_kkt_resgrad_ws_bytes(3, 1000, 1000) == 3 * (2 * 2000 + (4 + 4) * 1000 + 2 * 8) * 4
+    assert lib.iadmm_kkt_resgrad_ws_bytes(1, 24, 0) == (2 * 24 + 1 * 24 + 2 * 1) * 4
 
 
 def test_bad_arguments_rejected_before_launch():
