@@ -304,10 +304,19 @@ constexpr int tn_ring_floats() {
   return 3 * (16 * NA * 32 + 16 * 256) + ((NA * 2) % 4 ? 256 : 0);  // + the dummy-piece KiB
 }
 
+// The main loop issues no VALU work (gfx950: the fp32 MFMA shares the VALU datapath, every VALU
+// instruction beside it is matrix time lost; tools/mfma_valu_probe.hip):
+//   * each DMA piece keeps a loop-invariant per-lane voffset; the chunk's rows come in through a
+//     per-chunk descriptor (base at the chunk's first row, range ending at the split's last row:
+//     SALU only), so rows past the split read zero with no per-lane check;
+//   * the chunk loop is unrolled by the 3 ring stages, so every fragment read is a loop-invariant
+//     lane address + an immediate (stage 2 from its own lane bases: the ring is 78 KiB and the
+//     ds_read offset field reaches 64 KiB).
+// Same products in the same order as the r01 loop: bitwise the same slab.
 template <int NA>
 IADMM_DEV void gemm_tn_dma_body(int64_t M, int Ni, int No, int64_t rows_per_split, const float* X, const float* Y,
                                 float* slab, float* ring) {
-  constexpr int TI = NA * 32, SX = 16 * TI, SY = 16 * 256, NPX = NA * 2, XPW = (NPX + 3) / 4;
+  constexpr int TI = NA * 32, SX = 16 * TI, SY = 16 * 256, ST = SX + SY, NPX = NA * 2, XPW = (NPX + 3) / 4;
   const int tid = threadIdx.x, lane = tid & 63, jl = lane & 31, hf = lane >> 5;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int i0 = blockIdx.x * TI, o0 = blockIdx.y * 256;
@@ -322,14 +331,10 @@ IADMM_DEV void gemm_tn_dma_body(int64_t M, int Ni, int No, int64_t rows_per_spli
     for (int c = 0; c < 2; ++c)
 #pragma unroll
       for (int q = 0; q < 16; ++q) acc[a][c][q] = 0.f;
-  // panels start at row rbeg; the range ends at the split's last row
-  const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<float*>(X + rbeg * Ni), 0, (int)((int64_t)nrows * Ni * 4), 0x00020000);
-  const __amdgpu_buffer_rsrc_t yrs = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<float*>(Y + rbeg * No), 0, (int)((int64_t)nrows * No * 4), 0x00020000);
   // X piece p (wave p % 4) = stage floats [256p, 256p + 256): lane -> float 256p + 4*lane, i.e.
   // row / column of the [16][TI] image; a wave with no piece left issues an out-of-range dummy
-  // into the KiB after the ring.  Y piece q = stage row q, columns o0 + 4*lane .. +4.
+  // into the KiB after the ring.  Y piece q = stage row q, columns o0 + 4*lane .. +4.  Offsets are
+  // relative to the chunk's first row.
   unsigned xoff[XPW], yoff[4];
 #pragma unroll
   for (int i = 0; i < XPW; ++i) {
@@ -342,31 +347,58 @@ IADMM_DEV void gemm_tn_dma_body(int64_t M, int Ni, int No, int64_t rows_per_spli
     const int row = wave * 4 + i, col = o0 + lane * 4;
     yoff[i] = (col < No) ? (unsigned)(row * No + col) * 4u : 0x80000000u;
   }
-  auto issue = [&](int kc) {
-    float* sx = ring + (kc % 3) * (SX + SY);
+  auto issue = [&](int kc, auto S) {
+    constexpr int st = decltype(S)::value;
+    const int64_t r0 = rbeg + (int64_t)kc * 16;
+    const int left = nrows - kc * 16;  // >= 1: chunks are issued only below nk
+    const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(X + r0 * Ni), 0,
+                                                                          left * Ni * 4, 0x00020000);
+    const __amdgpu_buffer_rsrc_t yrs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(Y + r0 * No), 0,
+                                                                          left * No * 4, 0x00020000);
+    float* sx = ring + st * ST;
     float* sy = sx + SX;
-    const unsigned ox = (unsigned)(kc * 16 * Ni) * 4u, oy = (unsigned)(kc * 16 * No) * 4u;
 #pragma unroll
     for (int i = 0; i < XPW; ++i) {
       const int p = wave + 4 * i;
-      float* dst = (NPX % 4 == 0 || p < NPX) ? sx + p * 256 : ring + 3 * (SX + SY);
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(xrs, (lds_void*)dst, 16,
-                                               xoff[i] == 0x80000000u ? xoff[i] : xoff[i] + ox, 0, 0, 0);
+      float* dst = (NPX % 4 == 0 || p < NPX) ? sx + p * 256 : ring + 3 * ST;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(xrs, (lds_void*)dst, 16, xoff[i], 0, 0, 0);
     }
 #pragma unroll
     for (int i = 0; i < 4; ++i)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(yrs, (lds_void*)(sy + (wave * 4 + i) * 256), 16,
-                                               yoff[i] == 0x80000000u ? yoff[i] : yoff[i] + oy, 0, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(yrs, (lds_void*)(sy + (wave * 4 + i) * 256), 16, yoff[i], 0, 0, 0);
   };
-  // fragments of step ks (rows 2ks, 2ks+1) of chunk kc
-  auto frag = [&](int kc, int ks, float (&av)[NA], float (&bv)[2]) {
-    const float* sx = ring + (kc % 3) * (SX + SY);
-    const float* sy = sx + SX;
-    const int kk = 2 * ks + hf;
+  // fragment lane addresses (LDS bytes, ring base folded in): row kk = 2 ks + hf of the stage,
+  // X columns a*32 + jl, Y columns wave*64 + c*32 + jl; [1] = the same + stage 2's base.  One
+  // register per column block, laundered once per chunk: reads sharing a base register would be
+  // paired into ds_read2_b32, whose 8-bit offsets need a v_add per pair.
+  typedef __attribute__((address_space(3))) float lds_float;
+  typedef __attribute__((address_space(3))) const float lds_cfloat;
+  const unsigned rb = (unsigned)(uintptr_t)(lds_float*)ring;
+  unsigned xb[2][NA], yb[2][2];
 #pragma unroll
-    for (int a = 0; a < NA; ++a) av[a] = sx[kk * TI + a * 32 + jl];
+  for (int g = 0; g < 2; ++g) {
 #pragma unroll
-    for (int c = 0; c < 2; ++c) bv[c] = sy[kk * 256 + wave * 64 + c * 32 + jl];
+    for (int a = 0; a < NA; ++a) xb[g][a] = rb + (unsigned)(g * 2 * ST + hf * TI + a * 32 + jl) * 4u;
+#pragma unroll
+    for (int c = 0; c < 2; ++c) yb[g][c] = rb + (unsigned)(g * 2 * ST + SX + hf * 256 + wave * 64 + c * 32 + jl) * 4u;
+  }
+  auto launder = [&] {
+#pragma unroll
+    for (int g = 0; g < 2; ++g) {
+#pragma unroll
+      for (int a = 0; a < NA; ++a) asm volatile("" : "+v"(xb[g][a]));
+      asm volatile("" : "+v"(yb[g][0]), "+v"(yb[g][1]));
+    }
+  };
+  auto ld = [](unsigned addr) -> float { return *(lds_cfloat*)(uintptr_t)addr; };
+  auto frag = [&](auto S, int ks, float (&av)[NA], float (&bv)[2]) {
+    constexpr int st = decltype(S)::value;
+    constexpr int g = st == 2;
+    constexpr unsigned so = st == 2 ? 0u : st * ST * 4u;
+#pragma unroll
+    for (int a = 0; a < NA; ++a) av[a] = ld(xb[g][a] + so + (unsigned)(2 * ks * TI) * 4u);
+#pragma unroll
+    for (int c = 0; c < 2; ++c) bv[c] = ld(yb[g][c] + so + (unsigned)(2 * ks * 256) * 4u);
   };
   // A wave whose 64 output columns all lie past No (the last o tile when No % 256 != 0, e.g. the
   // half-empty 13th tile of No = 4h = 3200) skips its MFMAs: its SIMD's matrix pipe goes to the
@@ -380,41 +412,52 @@ IADMM_DEV void gemm_tn_dma_body(int64_t M, int Ni, int No, int64_t rows_per_spli
       for (int c = 0; c < 2; ++c)
         acc[a][c] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[a], bv[c], acc[a][c], 0, 0, 0);
   };
+  float av0[NA], bv0[2], av1[NA], bv1[2];
   // One barrier per chunk, after its first half: each wave has waited for its own pieces of chunk
   // kc+1 (chunk kc+2 not yet issued), so after the barrier chunk kc+1 is readable and the stage of
   // chunk kc-1 is free for chunk kc+2.  The first fragments of chunk kc+1 are read during the
   // second half of chunk kc, so no chunk starts on an LDS-latency stall.
-  issue(0);
-  if (nk > 1) issue(1);
-  if (nk > 1) vm_wait<XPW + 4>(); else vm_wait<0>();
-  __builtin_amdgcn_s_barrier();
-  float av0[NA], bv0[2], av1[NA], bv1[2];
-  frag(0, 0, av0, bv0);
-  for (int kc = 0; kc < nk; ++kc) {
+  auto step = [&](int kc, auto S) {
+    constexpr int st = decltype(S)::value;
+    launder();
 #pragma unroll
     for (int ks = 0; ks < 4; ks += 2) {
-      frag(kc, ks + 1, av1, bv1);
+      frag(S, ks + 1, av1, bv1);
       mma(av0, bv0);
-      frag(kc, ks + 2, av0, bv0);
+      frag(S, ks + 2, av0, bv0);
       mma(av1, bv1);
     }
     __builtin_amdgcn_sched_barrier(0);
-    if (kc + 1 < nk) {
+    const bool more = kc + 1 < nk;
+    if (more) {
       vm_wait<0>();
       __builtin_amdgcn_s_barrier();
       __builtin_amdgcn_sched_barrier(0);
-      if (kc + 2 < nk) issue(kc + 2);
+      if (kc + 2 < nk) issue(kc + 2, Stage<(st + 2) % 3>{});
     }
 #pragma unroll
     for (int ks = 4; ks < 8; ks += 2) {
-      frag(kc, ks + 1, av1, bv1);
+      frag(S, ks + 1, av1, bv1);
       mma(av0, bv0);
-      if (ks + 2 < 8) frag(kc, ks + 2, av0, bv0);
-      else if (kc + 1 < nk) frag(kc + 1, 0, av0, bv0);
+      if (ks + 2 < 8) frag(S, ks + 2, av0, bv0);
+      else if (more) frag(Stage<(st + 1) % 3>{}, 0, av0, bv0);
       mma(av1, bv1);
     }
     __builtin_amdgcn_sched_barrier(0);
+  };
+  issue(0, Stage<0>{});
+  if (nk > 1) issue(1, Stage<1>{});
+  if (nk > 1) vm_wait<XPW + 4>(); else vm_wait<0>();
+  __builtin_amdgcn_s_barrier();
+  frag(Stage<0>{}, 0, av0, bv0);
+  int kc = 0;
+  for (; kc + 3 <= nk; kc += 3) {  // one exit: the chunk index stays scalar
+    step(kc, Stage<0>{});
+    step(kc + 1, Stage<1>{});
+    step(kc + 2, Stage<2>{});
   }
+  if (kc < nk) step(kc, Stage<0>{});
+  if (kc + 1 < nk) step(kc + 1, Stage<1>{});
   float* S = slab + (int64_t)blockIdx.z * Ni * No;
 #pragma unroll
   for (int a = 0; a < NA; ++a)
