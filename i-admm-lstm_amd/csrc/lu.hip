@@ -22,8 +22,9 @@
 // (U) substitution: 64-row blocks, prefix dot products over coalesced row segments, the 64x64
 // diagonal block solved inside one wave.
 //
-// Pivots are stored 0-based (global row index swapped with row i).  info[b] = first i+1 with a
-// zero pivot (0 = non-singular), LAPACK convention.
+// Pivots are stored 1-based, LAPACK / torch.linalg.lu_factor convention (row i was swapped with
+// row piv[i]-1), so (LU, piv) also feeds torch.linalg.lu_solve.  info[b] = first i+1 with a zero
+// pivot (0 = non-singular), LAPACK convention.
 #include <algorithm>
 #include <type_traits>
 
@@ -165,7 +166,7 @@ __global__ __launch_bounds__(NT, NT <= 256 ? 2 : 1) void lu_panel_kernel(int N, 
         if (bx >= R) bx = j;  // all entries NaN: keep the diagonal
         else if (bv == 0.f && info[b] == 0) info[b] = k0 + j + 1;
         ri[NWV] = bx;
-        piv[b * N + k0 + j] = k0 + bx;
+        piv[b * N + k0 + j] = k0 + bx + 1;
         pvs[j] = k0 + bx;
       }
       __syncthreads();
@@ -308,7 +309,7 @@ __global__ __launch_bounds__(64) void lu_block_perm_kernel(int N, int K0, int ce
   __shared__ int pvs[kBlk], prow[2 * kBlk], pcur[2 * kBlk], pcnt[1];
   const int tid = threadIdx.x, nbk = cend - K0;
   const size_t b = blockIdx.x;
-  if (tid < nbk) pvs[tid] = piv[b * N + K0 + tid];
+  if (tid < nbk) pvs[tid] = piv[b * N + K0 + tid] - 1;
   __syncthreads();
   build_row_perm(pvs, K0, nbk, prow, pcur, pcnt);
   int* out = perm + b * kPermInts;
@@ -536,7 +537,7 @@ __global__ __launch_bounds__(kSolveThreads) void lu_solve_kernel(int N, const fl
   __syncthreads();
   if (tid == 0) {
     for (int i = 0; i < N; ++i) {
-      const int p = piv[b * N + i];
+      const int p = piv[b * N + i] - 1;
       if (p != i) { const float t = x[i]; x[i] = x[p]; x[p] = t; }
     }
   }

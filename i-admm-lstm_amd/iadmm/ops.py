@@ -249,7 +249,7 @@ def kkt_rhs(p, x, y, z, sigma, scal=None, num_ineq=0, rho_rows=None, out=None):
 
 
 def lu_factor(K):
-    """In-place batched LU with partial pivoting: returns (LU (= K), piv int32 [B,N], info int32 [B])."""
+    """In-place batched LU with partial pivoting: returns (LU (= K), piv int32 [B,N] 1-based (LAPACK), info int32 [B])."""
     B, N = K.shape[0], K.shape[1]
     piv = torch.empty(B, N, dtype=torch.int32, device=K.device)
     info = torch.empty(B, dtype=torch.int32, device=K.device)

@@ -105,7 +105,8 @@ int iadmm_kkt_rhs(int64_t B, int64_t n, int64_t m, int64_t num_ineq, const float
                   const float* scal, const float* rho_rows, float* out, void* stream);
 
 /* Stage II batched LU with partial pivoting, in place (replaces torch.lu, models/lu.py:31):
- * A[B,N,N] -> packed L\U; piv[B,N] int32, 0-based (row i was swapped with piv[i]);
+ * A[B,N,N] -> packed L\U; piv[B,N] int32, 1-based like LAPACK getrf / torch.linalg.lu_factor
+ * (row i was swapped with row piv[i]-1);
  * info[B] = first 1-based zero pivot or 0.  Right-looking in 64-column blocks (16-column panels up to N = 2048,
  * 8-column panels on 1024-thread workgroups above; rank-64 MFMA trailing update; limit N <= 10240).  Uses a B x 257-int stream-ordered scratch
  * (hipMallocAsync / hipFreeAsync on `stream`). */

@@ -5,8 +5,8 @@ First call (``lu is None and piv is None``): the dense K is assembled on the dev
 blocked LU kernel (iadmm_lu_factor) and solved (iadmm_lu_solve); later calls reuse (lu, piv).
 The x/z/y update runs with the fixed alpha = 1.6 relaxation on x AND z (iadmm_admm_update,
 relax_z).  Returns the reference's 8-tuple; ``A_tild`` is a lazy KKT operator carrying the same
-rho (``torch.bmm(A_tild, xv)`` works, ``.dense()`` materialises it) and ``piv`` holds 0-based
-int32 row interchanges (LAPACK uses 1-based; the tuple is opaque to the reference's caller).
+rho (``torch.bmm(A_tild, xv)`` works, ``.dense()`` materialises it) and ``piv`` holds 1-based
+int32 row interchanges like ``torch.lu`` / LAPACK, so (lu, piv) also feed ``torch.linalg.lu_solve``.
 A singular K raises like ``torch.lu`` does.
 """
 import torch
