@@ -229,6 +229,18 @@ def load_weights(args, h, T):
     return params, "trained:" + os.path.relpath(path, ROOT)
 
 
+def launch_ranks(args):
+    """``python bench.py --gpus N`` with no launcher around it and N > 1: run N ranks under
+    torch.distributed.run as a child process and exit with its status (iadmm/launch.py; nothing
+    here has touched the GPU yet).  Under a launcher, WORLD_SIZE must equal --gpus."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location(
+        "iadmm_launch", os.path.join(ROOT, "i-admm-lstm_amd", "iadmm", "launch.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    mod.relaunch(os.path.abspath(sys.argv[0]), sys.argv[1:], args.gpus)
+
+
 def heartbeat(period_s=60.0):
     """Print a progress line to stderr every ``period_s`` while a long step runs (config 4 takes
     minutes per step; a silent process looks hung to a supervisor)."""
@@ -245,6 +257,7 @@ def heartbeat(period_s=60.0):
 
 def main():
     args = parse()
+    launch_ranks(args)
     heartbeat()
     from iadmm import data, parallel, solver
     world, rank, local = parallel.env()

@@ -5,7 +5,8 @@ and the per-kernel time split from rocprof-compatible hipEvents.  Not the headli
 (bench.py is); this measures row a12.
 
   python bench_train.py --batch 32 --micro_batch 32 --outer_T 100      # per GPU
-  python -m torch.distributed.run --nproc-per-node 8 bench_train.py --batch 512 --micro_batch 32
+  python bench_train.py --gpus 8 --batch 512 --micro_batch 128      # starts 8 ranks itself
+  python -m torch.distributed.run --nproc-per-node 8 bench_train.py --gpus 8 --batch 512 --micro_batch 128
 """
 import argparse
 import json
@@ -20,8 +21,20 @@ sys.path.insert(0, ROOT)
 import torch  # noqa: E402
 
 
+def launch_ranks(args):
+    """N > 1 ranks without a launcher: torch.distributed.run child (iadmm/launch.py, loaded by
+    path before anything touches the GPU), exit with its status; see bench.launch_ranks."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location(
+        "iadmm_launch", os.path.join(ROOT, "i-admm-lstm_amd", "iadmm", "launch.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    mod.relaunch(os.path.abspath(sys.argv[0]), sys.argv[1:], args.gpus)
+
+
 def main():
     ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1, help="ranks (one per GPU); started here when no launcher did")
     ap.add_argument("--batch", type=int, default=32, help="instances per GPU")
     ap.add_argument("--micro_batch", type=int, default=32)
     ap.add_argument("--num_var", type=int, default=1000)
@@ -32,6 +45,7 @@ def main():
     ap.add_argument("--steps", type=int, default=2)
     ap.add_argument("--warmup", type=int, default=1)
     args = ap.parse_args()
+    launch_ranks(args)
     from iadmm import data, ops, parallel, train
     from models.lstm import LSTM
     world, rank, local = parallel.env()

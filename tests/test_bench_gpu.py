@@ -32,7 +32,7 @@ def _run(args, nproc=1, timeout=600, shared=True, extra_env=None, launcher=False
         env["IADMM_SHARED_GPU"] = "1"
     if nproc > 1 or launcher:
         cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
-               "--master-addr", "127.0.0.1", "--master-port", str(_free_port())] + args
+               "--master-addr", "127.0.0.1", "--master-port", str(_free_port())] + args + ["--gpus", str(nproc)]
     else:
         cmd = [sys.executable] + args
     out = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=timeout)
@@ -82,6 +82,33 @@ def test_bench_train_two_ranks_shared_gpu():
     assert r["n_gpus"] == 2 and r["value"] > 0 and r["loss"] == r["loss"]
 
 
+def test_bench_gpus_flag_starts_the_ranks():
+    """The driver's command form: plain `python bench.py --gpus 2` (no launcher) must run two ranks
+    (here sharing cuda:0 over gloo) and report n_gpus 2 over the doubled global batch."""
+    env = dict(os.environ, IADMM_SHARED_GPU="1")
+    env.pop("WORLD_SIZE", None)
+    out = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--batch", "4", "--steps", "1", "--warmup", "0",
+                          "--cpu-sample", "0", "--stage2-iters", "0", "--alt-f16x3", "0"] + SMALL,
+                         cwd=ROOT, env=env, capture_output=True, text=True, timeout=600)
+    assert out.returncode == 0, out.stderr[-3000:]
+    lines = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, out.stdout[-2000:]
+    r = json.loads(lines[0])
+    assert r["n_gpus"] == 2 and r["config"]["global_batch"] == 8 and r["dist_backend"] == "gloo"
+
+
+def test_bench_train_gpus_flag_starts_the_ranks():
+    env = dict(os.environ, IADMM_SHARED_GPU="1")
+    env.pop("WORLD_SIZE", None)
+    out = subprocess.run([sys.executable, "bench_train.py", "--gpus", "2", "--batch", "2", "--micro_batch", "1",
+                          "--steps", "1", "--warmup", "0", "--num_var", "32", "--num_ineq", "16", "--num_eq", "16",
+                          "--hidden_dim", "32", "--outer_T", "2"],
+                         cwd=ROOT, env=env, capture_output=True, text=True, timeout=600)
+    assert out.returncode == 0, out.stderr[-3000:]
+    r = json.loads([ln for ln in out.stdout.splitlines() if ln.startswith("{")][-1])
+    assert r["n_gpus"] == 2 and r["dist_backend"] == "gloo" and r["allreduce_calls"] >= 1
+
+
 def _need_two_gpus():
     if torch.cuda.device_count() < 2:
         pytest.skip("the RCCL path needs >= 2 GPUs (one rank per GPU)")
@@ -94,6 +121,20 @@ def test_bench_two_ranks_rccl():
     r = _run(["bench.py", "--batch", "4", "--steps", "1", "--warmup", "0", "--cpu-sample", "0"] + SMALL, nproc=2,
              shared=False)
     assert r["n_gpus"] == 2 and r["config"]["global_batch"] == 8 and r["value"] > 0
+
+
+def test_bench_gpus_flag_rccl():
+    """`python bench.py --gpus 2` on a multi-GPU node: one rank per GPU over RCCL."""
+    _need_two_gpus()
+    env = dict(os.environ)
+    env.pop("WORLD_SIZE", None)
+    env.pop("IADMM_SHARED_GPU", None)
+    out = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--batch", "4", "--steps", "1", "--warmup", "0",
+                          "--cpu-sample", "0", "--stage2-iters", "0", "--alt-f16x3", "0"] + SMALL,
+                         cwd=ROOT, env=env, capture_output=True, text=True, timeout=600)
+    assert out.returncode == 0, out.stderr[-3000:]
+    r = json.loads([ln for ln in out.stdout.splitlines() if ln.startswith("{")][-1])
+    assert r["n_gpus"] == 2 and r["config"]["global_batch"] == 8 and r["dist_backend"] == "nccl"
 
 
 def test_bench_train_two_ranks_rccl():
