@@ -703,20 +703,25 @@ static int lu_factor_blocks(int64_t B, int64_t N, float* A, int* piv, int* info,
   return 0;
 }
 
-extern "C" int iadmm_lu_factor(int64_t B, int64_t N, float* A, int* piv, int* info, void* stream) {
-  if (B <= 0 || N <= 0 || !A || !piv || !info) return IADMM_E_ARG;
+static int64_t lu_ws_bytes(int64_t B) { return B * (int64_t)kPermInts * (int64_t)sizeof(int); }
+
+extern "C" int64_t iadmm_lu_factor_ws_bytes(int64_t B, int64_t N) {
+  if (B <= 0 || N <= 0) return 0;
+  return lu_ws_bytes(B);
+}
+
+extern "C" int iadmm_lu_factor(int64_t B, int64_t N, float* A, int* piv, int* info, void* ws, int64_t ws_bytes,
+                               void* stream) {
+  if (B <= 0 || N <= 0 || !A || !piv || !info || !ws) return IADMM_E_ARG;
+  if (ws_bytes < lu_ws_bytes(B)) return IADMM_E_ARG;
+  if (!aligned16(ws)) return IADMM_E_ALIGN;
   if (N > kBigMaxM * kBigThreads || B > 0x7fffffff) return IADMM_E_SIZE;
-  hipStream_t s = (hipStream_t)stream;
-  hipError_t e = hipMemsetAsync(info, 0, B * sizeof(int), s);
-  if (e != hipSuccess) return (int)e;
   const int64_t ntc_max = (N + kTC - 1) / kTC, nrc_max = (N + kTRW - 1) / kTRW;
   if (B * ntc_max * nrc_max > 0x7fffffff) return IADMM_E_SIZE;
-  int* perm = nullptr;  // per-instance block permutations (stream-ordered scratch)
-  e = hipMallocAsync((void**)&perm, (size_t)B * kPermInts * sizeof(int), s);
+  hipStream_t s = (hipStream_t)stream;
+  const hipError_t e = hipMemsetAsync(info, 0, B * sizeof(int), s);
   if (e != hipSuccess) return (int)e;
-  const int rc = lu_factor_blocks(B, N, A, piv, info, perm, s);
-  e = hipFreeAsync(perm, s);
-  return rc != 0 ? rc : (int)e;
+  return lu_factor_blocks(B, N, A, piv, info, static_cast<int*>(ws), s);  // ws: per-instance block permutations
 }
 
 extern "C" int iadmm_lu_solve(int64_t B, int64_t N, const float* LU, const int* piv, float* x,

@@ -248,12 +248,22 @@ def kkt_rhs(p, x, y, z, sigma, scal=None, num_ineq=0, rho_rows=None, out=None):
     return out
 
 
-def lu_factor(K):
-    """In-place batched LU with partial pivoting: returns (LU (= K), piv int32 [B,N] 1-based (LAPACK), info int32 [B])."""
+def lu_factor_ws(B, N, device):
+    """Workspace of iadmm_lu_factor (caller-owned, from the PyTorch caching allocator)."""
+    nbytes = int(_abi.lib().iadmm_lu_factor_ws_bytes(int(B), int(N)))
+    return torch.empty((nbytes + 3) // 4, dtype=torch.float32, device=device)
+
+
+def lu_factor(K, ws=None):
+    """In-place batched LU with partial pivoting: returns (LU (= K), piv int32 [B,N] 1-based (LAPACK), info int32 [B]).
+    ``ws``: a :func:`lu_factor_ws` buffer (allocated per call when omitted)."""
+    if K.dim() != 3 or K.shape[1] != K.shape[2]:
+        raise ValueError(f"K must be [B,N,N], got {tuple(K.shape)}")
     B, N = K.shape[0], K.shape[1]
     piv = torch.empty(B, N, dtype=torch.int32, device=K.device)
     info = torch.empty(B, dtype=torch.int32, device=K.device)
-    _abi.call("iadmm_lu_factor", B, N, _p(K), piv.data_ptr(), info.data_ptr(), _stream())
+    ws = lu_factor_ws(B, N, K.device) if ws is None else ws
+    _abi.call("iadmm_lu_factor", B, N, _p(K), piv.data_ptr(), info.data_ptr(), _p(ws), ws.numel() * 4, _stream())
     return K, piv, info
 
 

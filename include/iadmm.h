@@ -108,9 +108,12 @@ int iadmm_kkt_rhs(int64_t B, int64_t n, int64_t m, int64_t num_ineq, const float
  * A[B,N,N] -> packed L\U; piv[B,N] int32, 1-based like LAPACK getrf / torch.linalg.lu_factor
  * (row i was swapped with row piv[i]-1);
  * info[B] = first 1-based zero pivot or 0.  Right-looking in 64-column blocks (16-column panels up to N = 2048,
- * 8-column panels on 1024-thread workgroups above; rank-64 MFMA trailing update; limit N <= 10240).  Uses a B x 257-int stream-ordered scratch
- * (hipMallocAsync / hipFreeAsync on `stream`). */
-int iadmm_lu_factor(int64_t B, int64_t N, float* A, int* piv, int* info, void* stream);
+ * 8-column panels on 1024-thread workgroups above; MFMA trailing update; limit N <= 10240).
+ * ws: caller-owned, 16-B aligned device workspace of at least iadmm_lu_factor_ws_bytes(B, N) bytes
+ * (per-instance block permutations); nothing is allocated inside. */
+int64_t iadmm_lu_factor_ws_bytes(int64_t B, int64_t N);
+int iadmm_lu_factor(int64_t B, int64_t N, float* A, int* piv, int* info, void* ws, int64_t ws_bytes,
+                    void* stream);
 
 /* Solve with the factors in place (replaces torch.lu_solve, models/lu.py:32,35): x[B,N] holds b
  * on entry and the solution on exit.  Limit: (N + 4224) floats of LDS <= 160 KiB, N <= 36736. */

@@ -58,3 +58,28 @@ def test_bad_arguments_rejected_before_launch():
                   None)
     with pytest.raises(_abi.IadmmError, match="bad argument"):
         _abi.call("iadmm_lstm_cell_fwd", 10, 8, 16, 16, 16, 16, 16, 16, 16, 16, 16, None)
+
+
+def test_lu_factor_workspace_is_caller_owned():
+    """iadmm_lu_factor takes its scratch from the caller (no allocation inside the
+    library): the size query answers without a GPU and a missing or short workspace is refused."""
+    lib = _abi.lib()
+    assert lib.iadmm_lu_factor_ws_bytes(1024, 2000) >= 1024 * (4 * 64 + 1) * 4
+    assert lib.iadmm_lu_factor_ws_bytes(0, 2000) == 0
+    need = lib.iadmm_lu_factor_ws_bytes(2, 100)
+    with pytest.raises(_abi.IadmmError, match="bad argument"):
+        _abi.call("iadmm_lu_factor", 2, 100, 16, 16, 16, None, need, None)
+    with pytest.raises(_abi.IadmmError, match="bad argument"):
+        _abi.call("iadmm_lu_factor", 2, 100, 16, 16, 16, 16, need - 4, None)
+    with pytest.raises(_abi.IadmmError, match="misaligned"):
+        _abi.call("iadmm_lu_factor", 2, 100, 16, 16, 16, 20, need, None)
+
+
+def test_no_device_allocation_inside_the_library():
+    """Every device buffer is caller-owned: no hipMalloc* / hipFree* call in the HIP sources."""
+    csrc = os.path.join(REPO, "i-admm-lstm_amd", "csrc")
+    hits = []
+    for fn in sorted(os.listdir(csrc)):
+        src = re.sub(r"//[^\n]*|/\*.*?\*/", "", open(os.path.join(csrc, fn)).read(), flags=re.S)
+        hits += [f"{fn}: {m.group(0)}" for m in re.finditer(r"\bhip(Malloc|Free)\w*", src)]
+    assert not hits, hits
