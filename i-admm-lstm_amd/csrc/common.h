@@ -43,7 +43,10 @@ IADMM_DEV float sigmoidf_(float x) { return 1.0f / (1.0f + expf(-x)); }
 //            error (5e-9 in exact arithmetic, <= ~6 ulp evaluated in fp32): relative accuracy down
 //            to 0 (small LSTM states), no exp, no select
 // The sigmoid needs no clamp: 2^(+inf) = inf -> rcp = 0, 2^(-inf) = 0 -> rcp(1) = 1, so it
-// saturates to 0 / 1 like torch and NaN propagates; tanh saturates through its clamp.
+// saturates to 0 / 1 like torch and NaN propagates; tanh saturates through its clamp, and a NaN
+// input is passed through explicitly (v_med3 with a NaN operand returns min3 of its operands, i.e.
+// the clamp would turn tanh(NaN) into tanh(-7.9) = -1 and hide a divergent solve; torch.tanh
+// propagates NaN: one compare + select per element, r03).
 // Why so lean: on gfx950 v_mfma_f32_32x32x2_f32 runs on the fp32 VALU datapath, so every VALU
 // cycle of the epilogue is a cycle the SIMD's matrix work stalls (tools/mfma_valu_probe.hip,
 // profiles/r02_mfma_valu_probe.txt).  The r01 forms (Cody-Waite exp with a v_med3 clamp, tanh as a
@@ -56,8 +59,8 @@ constexpr float kTp1 = 0.1313343644142151f, kTp2 = 0.0031596473418176174f, kTp3 
 constexpr float kTq1 = 0.4646677076816559f, kTq2 = 0.024715565145015717f, kTq3 = 0.00026282211183570325f;
 
 IADMM_DEV float sigmoid_cell(float x) { return __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(x * kNL2E)); }
-IADMM_DEV float tanh_cell(float x) {
-  x = __builtin_amdgcn_fmed3f(x, -kTanhClamp, kTanhClamp);
+IADMM_DEV float tanh_cell(float x0) {
+  const float x = __builtin_amdgcn_fmed3f(x0, -kTanhClamp, kTanhClamp);
   const float s = x * x;
   float p = fmaf(s, kTp6, kTp5);
   p = fmaf(s, p, kTp4);
@@ -68,7 +71,8 @@ IADMM_DEV float tanh_cell(float x) {
   float q = fmaf(s, kTq3, kTq2);
   q = fmaf(s, q, kTq1);
   q = fmaf(s, q, 1.0f);
-  return (x * p) * __builtin_amdgcn_rcpf(q);
+  const float r = (x * p) * __builtin_amdgcn_rcpf(q);
+  return x0 != x0 ? x0 : r;
 }
 // Gate pre-activation: (b + in0 w0 + in1 w1) + acc, i.e. inputs @ W + H @ U + b
 // (models/lstm.py:74-77) with the two-term input product on fmas.
@@ -81,8 +85,10 @@ IADMM_DEV float2v splat2(float v) { return float2v{v, v}; }
 IADMM_DEV float2v exp2_2(float2v y) { return float2v{__builtin_amdgcn_exp2f(y.x), __builtin_amdgcn_exp2f(y.y)}; }
 IADMM_DEV float2v rcp2(float2v d) { return float2v{__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)}; }
 IADMM_DEV float2v sigmoid_cell2(float2v x) { return rcp2(splat2(1.0f) + exp2_2(x * splat2(kNL2E))); }
-IADMM_DEV float2v tanh_cell2(float2v x) {
-  x = float2v{__builtin_amdgcn_fmed3f(x.x, -kTanhClamp, kTanhClamp), __builtin_amdgcn_fmed3f(x.y, -kTanhClamp, kTanhClamp)};
+IADMM_DEV float nan_pass(float x0, float r) { return x0 != x0 ? x0 : r; }
+IADMM_DEV float2v tanh_cell2(float2v x0) {
+  const float2v x = float2v{__builtin_amdgcn_fmed3f(x0.x, -kTanhClamp, kTanhClamp),
+                            __builtin_amdgcn_fmed3f(x0.y, -kTanhClamp, kTanhClamp)};
   const float2v s = x * x;
   float2v p = fma2(s, splat2(kTp6), splat2(kTp5));
   p = fma2(s, p, splat2(kTp4));
@@ -93,7 +99,8 @@ IADMM_DEV float2v tanh_cell2(float2v x) {
   float2v q = fma2(s, splat2(kTq3), splat2(kTq2));
   q = fma2(s, q, splat2(kTq1));
   q = fma2(s, q, splat2(1.0f));
-  return (x * p) * rcp2(q);
+  const float2v r = (x * p) * rcp2(q);
+  return float2v{nan_pass(x0.x, r.x), nan_pass(x0.y, r.y)};
 }
 // Four-lane forms (two unit pairs at once): every operation splits into two independent packed
 // halves, so dependent packed ops never sit back to back (no s_nop hazard padding) and the
@@ -110,9 +117,11 @@ IADMM_DEV float4v rcp4(float4v d) {
                  __builtin_amdgcn_rcpf(d.w)};
 }
 IADMM_DEV float4v sigmoid_cell4(float4v x) { return rcp4(splat4(1.0f) + exp2_4(x * splat4(kNL2E))); }
-IADMM_DEV float4v tanh_cell4(float4v x) {
-  x = float4v{__builtin_amdgcn_fmed3f(x.x, -kTanhClamp, kTanhClamp), __builtin_amdgcn_fmed3f(x.y, -kTanhClamp, kTanhClamp),
-              __builtin_amdgcn_fmed3f(x.z, -kTanhClamp, kTanhClamp), __builtin_amdgcn_fmed3f(x.w, -kTanhClamp, kTanhClamp)};
+IADMM_DEV float4v tanh_cell4(float4v x0) {
+  const float4v x = float4v{__builtin_amdgcn_fmed3f(x0.x, -kTanhClamp, kTanhClamp),
+                            __builtin_amdgcn_fmed3f(x0.y, -kTanhClamp, kTanhClamp),
+                            __builtin_amdgcn_fmed3f(x0.z, -kTanhClamp, kTanhClamp),
+                            __builtin_amdgcn_fmed3f(x0.w, -kTanhClamp, kTanhClamp)};
   const float4v s = x * x;
   float4v p = fma4(s, splat4(kTp6), splat4(kTp5));
   p = fma4(s, p, splat4(kTp4));
@@ -123,7 +132,8 @@ IADMM_DEV float4v tanh_cell4(float4v x) {
   float4v q = fma4(s, splat4(kTq3), splat4(kTq2));
   q = fma4(s, q, splat4(kTq1));
   q = fma4(s, q, splat4(1.0f));
-  return (x * p) * rcp4(q);
+  const float4v r = (x * p) * rcp4(q);
+  return float4v{nan_pass(x0.x, r.x), nan_pass(x0.y, r.y), nan_pass(x0.z, r.z), nan_pass(x0.w, r.w)};
 }
 IADMM_DEV float4v cell_pre4(float4v in0, float4v in1, float4v acc, float4v w0, float4v w1, float4v b) {
   return fma4(in1, w1, fma4(in0, w0, b)) + acc;

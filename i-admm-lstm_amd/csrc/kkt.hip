@@ -664,6 +664,22 @@ static int launch_combine(int pass, int64_t B, int nchunk, const KktSplitArgs& a
   return 0;
 }
 
+// LDS of the split sweeps: the two vectors (n + m floats) + one or two fold buffers of 4 panel
+// rows each (two while the total stays within IADMM_KKT_DBUF_BYTES, so that at least two
+// workgroups share a CU; one otherwise); panel width = min(n, 256 NG).
+static int64_t split_lds_bytes(int64_t n, int64_t m, bool* dbuf_out) {
+  const int ng = ng_for(n < kPanelNG * 256 ? n : kPanelNG * 256);
+  const int64_t fstride = split_fstride((int)n, ng * 256);
+  const bool dbuf = (n + m + 8 * fstride) * 4 <= IADMM_KKT_DBUF_BYTES;
+  if (dbuf_out) *dbuf_out = dbuf;
+  return (n + m + (dbuf ? 8 : 4) * fstride) * (int64_t)sizeof(float);
+}
+
+extern "C" int64_t iadmm_kkt_resgrad_lds_bytes(int64_t n, int64_t m) {
+  if (n <= 0 || m < 0 || n > 0x7fffffff || m > 0x7fffffff) return 0;
+  return split_lds_bytes(n, m, nullptr);
+}
+
 // The row-block split pipeline p1 -> c1 -> [p2] -> c2 for one of the three modes.  ``a`` carries
 // the mode's inputs/outputs; the geometry, workspace carving and pass-1 vector are filled here.
 static int run_split(int mode, int64_t B, int64_t n, int64_t m, KktSplitArgs a, void* ws, int64_t ws_bytes,
@@ -671,12 +687,8 @@ static int run_split(int mode, int64_t B, int64_t n, int64_t m, KktSplitArgs a, 
   if (!ws || ws_bytes < iadmm_kkt_resgrad_ws_bytes(B, n, m) || !aligned16(ws)) return IADMM_E_ARG;
   const int64_t nbq = (n + kRB - 1) / kRB, nba = (m + kRB - 1) / kRB, nblk = nbq + nba;
   const int ng = ng_for(n < kPanelNG * 256 ? n : kPanelNG * 256);
-  // LDS: the two vectors + one or two fold buffers (two while the total stays within 64 KiB, so
-  // that at least two workgroups share a CU; one otherwise)
-  const int64_t fstride = split_fstride((int)n, ng * 256);
-  const int64_t vec_floats = n + m;
-  const bool dbuf = (vec_floats + 8 * fstride) * 4 <= IADMM_KKT_DBUF_BYTES;
-  const size_t lds = (vec_floats + (dbuf ? 8 : 4) * fstride) * sizeof(float);
+  bool dbuf = false;
+  const int64_t lds = split_lds_bytes(n, m, &dbuf);
   if (lds > 160 * 1024 || B > 0x7fffffff) return IADMM_E_SIZE;
   // workgroups per instance: the batch's workgroups fill the chip's resident slots (4 per CU x
   // 256 CUs) in ONE round -- a second, partial round of long streaming workgroups idles most of

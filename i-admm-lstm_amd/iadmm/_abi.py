@@ -20,6 +20,7 @@ SIGNATURES = {
     "iadmm_schedule": (cint, [vp, vp, i64, vp, vp]),
     "iadmm_schedule_fixed_alpha": (cint, [vp, f32, vp, vp]),
     "iadmm_kkt_resgrad_ws_bytes": (i64, [i64, i64, i64]),
+    "iadmm_kkt_resgrad_lds_bytes": (i64, [i64, i64]),
     "iadmm_kkt_resgrad": (cint, [i64, i64, i64, i64, vp, vp, vp, vp, vp, vp, vp, f32, vp, vp, vp, vp, vp, vp, i64,
                                  vp]),
     "iadmm_kkt_lsres": (cint, [i64, i64, i64, i64, vp, vp, vp, vp, vp, vp, vp, f32, vp, vp, vp]),

@@ -190,7 +190,7 @@ def solve(params, Q, p, A0, zl, zu, num_ineq, num_eq, T, sigma, scaling=True, sc
     timer.stop(tok)
 
     # state (two sets) and work buffers
-    tok = timer.start("setup")
+    tok = timer.start("untimed:setup")  # the reference allocates its zeros before start_time (main.py:836-841)
     xs = [torch.zeros(B, n, **f32), torch.empty(B, n, **f32)]
     ys = [torch.zeros(B, m, **f32), torch.empty(B, m, **f32)]
     zs = [torch.zeros(B, m, **f32), torch.empty(B, m, **f32)]
@@ -302,7 +302,7 @@ def solve(params, Q, p, A0, zl, zu, num_ineq, num_eq, T, sigma, scaling=True, sc
         x, y, z = xs[cur], ys[cur], zs[cur]
     timer.stop(tok)
 
-    tok = timer.start("metrics")
+    tok = timer.start("untimed:metrics")  # the reference times no metric work (main.py:949-978)
     obj, pr, du = _metrics(Q, p, A0, Qs, ps, As, D, E, c, x, y, z, xs[cur], ys[cur], zs[cur],
                            keep_unscaled or not scaling)
     timer.stop(tok)

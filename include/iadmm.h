@@ -70,8 +70,11 @@ int iadmm_schedule_fixed_alpha(const float* scal_in, float alpha, float* scal_ou
  * the chip at any B; column sums are combined per block in block order, so g does not depend on
  * B (or on how a batch is sharded).  ws: caller-owned, 16-B aligned device workspace of at least
  * iadmm_kkt_resgrad_ws_bytes(B, n, m) bytes (the same size serves iadmm_kkt_bwd_split and
- * iadmm_loss_grad_split).  Limit: 2n + m floats of LDS <= 160 KiB. */
+ * iadmm_loss_grad_split).  Limit: iadmm_kkt_resgrad_lds_bytes(n, m) <= 160 KiB (IADMM_E_SIZE
+ * otherwise); that is (n + m + k min(n, 2048)) floats with k = 8 while the sum stays within 64 KiB
+ * and k = 4 above (n = m = 1000: 39 KiB; n = m = 5000: 71 KiB; n = m <= 16384). */
 int64_t iadmm_kkt_resgrad_ws_bytes(int64_t B, int64_t n, int64_t m);
+int64_t iadmm_kkt_resgrad_lds_bytes(int64_t n, int64_t m);
 int iadmm_kkt_resgrad(int64_t B, int64_t n, int64_t m, int64_t num_ineq,
                       const float* Q, const float* A0, const float* p,
                       const float* x, const float* y, const float* z, const float* xv,

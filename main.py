@@ -225,8 +225,13 @@ def run_test(args):
 def timed_seconds(spans):
     """Parallel Time of one batch: the solver's timed spans (scaling, iterations, unscale, Stage II
     factor + iterations = the reference's timed model()/exact_model() calls, main.py:881-890,
-    1055-1066) without the per-kernel ("k:") and per-iteration metric ("hist:") spans."""
-    return sum(v for k, v in spans.items() if not k.startswith(("k:", "hist:"))) / 1e3
+    1055-1066) without the per-kernel ("k:"), per-iteration metric ("hist:") and untimed
+    ("untimed:": the state zero-fills, which the reference allocates before start_time,
+    main.py:836-841, and the final residual pass) spans."""
+    return sum(v for k, v in spans.items() if not k.startswith(UNTIMED_PREFIXES)) / 1e3
+
+
+UNTIMED_PREFIXES = ("k:", "hist:", "untimed:")
 
 
 COND_KEYS = ("x_cond_1_left", "x_cond_1_right", "x_cond_2_left", "x_cond_2_right", "z_cond_1_left",
@@ -271,23 +276,27 @@ def _instances(args, ids, device):
 def report_stats(d, x, mi, me, dist):
     """Objective and constraint violations of an unscaled iterate x [B,n] (main.py:367-379,
     497-516): obj mean, ineq/eq violation max-per-instance mean and elementwise mean.  With
-    ``dist`` the means are combined over ranks (each rank holds an equal share of the batch)."""
+    ``dist`` the sums and their counts (instances, elements) are all-reduced over ranks and then
+    divided, so unequal shards (parallel.shard differs by one instance) give the global-batch
+    means exactly."""
     B = x.shape[0]
     obj, _, _ = ops.metrics(d["Q"], d["p"].reshape(B, -1).contiguous(), d["A0"], x,
                             torch.zeros(B, d["A0"].shape[1], device=x.device),
                             torch.zeros(B, d["A0"].shape[1], device=x.device))
-    vals = [obj.mean()]
+    sums, counts = [obj.double().sum()], [B]
     if mi:
         iv = ops.bmv(d["G"].contiguous(), x, d["c"].reshape(B, -1).contiguous(), ops.BMV_POS_EXCESS)
-        vals += [iv.max(1).values.mean(), iv.mean()]
+        sums += [iv.max(1).values.double().sum(), iv.double().sum()]
+        counts += [B, iv.numel()]
     if me:
         ev = ops.bmv(d["A"].contiguous(), x, d["b"].reshape(B, -1).contiguous(), ops.BMV_ABS_GAP)
-        vals += [ev.max(1).values.mean(), ev.mean()]
-    t = torch.stack(vals).double()
+        sums += [ev.max(1).values.double().sum(), ev.double().sum()]
+        counts += [B, ev.numel()]
+    t = torch.cat([torch.stack(sums), torch.tensor(counts, dtype=torch.float64, device=x.device)])
     if dist is not None and dist.is_initialized() and dist.get_world_size() > 1:
         dist.all_reduce(t)
-        t /= dist.get_world_size()
-    t = t.tolist()
+    k = len(sums)
+    t = (t[:k] / t[k:]).tolist()
     out = {"obj": t.pop(0)}
     if mi:
         out["ineq_max"], out["ineq_mean"] = t.pop(0), t.pop(0)
@@ -324,22 +333,25 @@ def run_train(args):
         t0 = time.time()
         loss = float("nan")
         last = {}
-        for bi in range(int(len(train_ids) / args.batch_size)):
+        n_batches = int(len(train_ids) / args.batch_size)
+        for bi in range(n_batches):
             ids = train_ids[bi * args.batch_size:(bi + 1) * args.batch_size]
             first, count = parallel.shard(len(ids), world, rank)
             d = _instances(args, ids[first:first + count], device)
             Dsc = None
             if args.scaling:
-                Qs, ps, As, zls, zus, Dsc, _, _ = ops.ruiz_scale(d["Q"], d["p"], d["A0"], d["zl"], d["zu"],
-                                                                 args.scaling_ites)
-                ds = dict(Q=Qs, p=ps, A0=As, zl=zls, zu=zus)
+                sc = ops.ruiz_scale(d["Q"], d["p"], d["A0"], d["zl"], d["zu"], args.scaling_ites)
+                ds, Dsc = dict(zip(("Q", "p", "A0", "zl", "zu"), sc[:5])), sc[5]
+                del sc
             else:
                 ds = d
             fin = {}
             loss = train.tbptt_batch(model, ds, mi, me, args.outer_T, args.truncated_length, args.sigma, optimizer,
                                      micro_batch=args.micro_batch or None, global_batch=len(ids), dist=dist,
                                      final=fin)
-            last = dict(d=d, x=fin["x"].reshape(count, -1) * (Dsc.reshape(count, -1) if Dsc is not None else 1.0))
+            if bi == n_batches - 1:  # only the epoch's last batch is reported (main.py:362-379)
+                last = dict(d=d, x=fin["x"].reshape(count, -1) * (Dsc.reshape(count, -1) if Dsc is not None else 1.0))
+            del d, ds, fin
         train_time = time.time() - t0
         # main.py:362-379: objective and violations of the last training batch's final iterate
         # (unscaled); each rank holds its shard, so the means are combined over ranks

@@ -44,6 +44,14 @@ def test_size_queries_without_gpu():
     # partial sums per 256-row chunk of [n ; m]
     assert lib.iadmm_kkt_resgrad_ws_bytes(3, 1000, 1000) == 3 * (2 * 2000 + (4 + 4) * 1000 + 2 * 8) * 4
     assert lib.iadmm_kkt_resgrad_ws_bytes(1, 24, 0) == (2 * 24 + 1 * 24 + 2 * 1) * 4
+    # LDS of the split sweeps (the IADMM_E_SIZE limit): vectors + 8 fold rows below 64 KiB, 4 above
+    assert lib.iadmm_kkt_resgrad_lds_bytes(1000, 1000) == (2000 + 8 * 1000) * 4
+    assert lib.iadmm_kkt_resgrad_lds_bytes(5000, 5000) == (10000 + 4 * 2048) * 4
+    assert lib.iadmm_kkt_resgrad_lds_bytes(16384, 16384) == 160 * 1024
+
+
+def lib_lds_over(n, m):
+    return _abi.lib().iadmm_kkt_resgrad_lds_bytes(n, m) > 160 * 1024
 
 
 def test_bad_arguments_rejected_before_launch():
@@ -53,6 +61,7 @@ def test_bad_arguments_rejected_before_launch():
                   None)
     with pytest.raises(_abi.IadmmError, match="bad argument"):  # workspace missing / too small
         _abi.call("iadmm_kkt_resgrad", 2, 10, 10, 5, *([16] * 7), 1.0, 16, 16, None, None, None, 16, 100, None)
+    assert lib_lds_over(20000, 20000)
     with pytest.raises(_abi.IadmmError, match="size beyond"):
         _abi.call("iadmm_kkt_resgrad", 1, 20000, 20000, 0, *([16] * 7), 1.0, 16, 16, None, None, None, 16, 1 << 40,
                   None)

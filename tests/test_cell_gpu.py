@@ -95,3 +95,34 @@ def test_cell_saturated_gates(mag):
     assert float((Hn.double().cpu() - Href).abs()[ok].max()) < 1e-5
     fin = ok & (Cref.abs() < 1e30)
     assert rel(Cn.cpu()[fin], Cref[fin]) < 1e-5
+
+
+@pytest.mark.gpu
+def test_cell_propagates_nan_like_torch():
+    """A NaN gate pre-activation (inf * w0 - inf * w1 when xv and g overflow in a divergent solve)
+    or a NaN cell state must come out as NaN like torch.tanh gives it, not as a clamped tanh of
+    -7.9 = -1 (the v_med3 clamp returns min3 of its operands for a NaN input): the NaN patterns of
+    H' and C' equal the fp64 reference's, and every other entry matches it."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from iadmm import ops
+    M, h = 300, 40
+    gen = torch.Generator().manual_seed(9)
+    p = _params(h, 0.3, gen)
+    H = torch.tanh(torch.randn(M, h, generator=gen))
+    C = torch.randn(M, h, generator=gen)
+    C[7, 3] = float("nan")                      # a NaN cell state
+    xv, g = torch.randn(M, generator=gen), torch.randn(M, generator=gen)
+    xv[11], g[11] = float("inf"), float("inf")  # pre = inf w0 + inf w1: NaN where w0, w1 differ in sign
+    xv[12] = float("nan")                       # NaN input: every gate NaN
+    dev = {k: v.cuda() for k, v in p.items()}
+    Upk, Wx = ops.lstm_pack(dev, h)
+    Hn, Cn, _ = ops.lstm_cell(H.cuda(), C.cuda(), xv.cuda(), g.cuda(), Upk, Wx)
+    torch.cuda.synchronize()
+    Href, Cref, _ = _cell_fp64(p, H, C, xv, g)
+    Hn, Cn = Hn.cpu(), Cn.cpu()
+    assert torch.isnan(Href[11]).any() and not torch.isnan(Href[11]).all()  # the case is exercised
+    assert torch.equal(torch.isnan(Hn), torch.isnan(Href))
+    assert torch.equal(torch.isnan(Cn), torch.isnan(Cref))
+    fin = torch.isfinite(Href)
+    assert float((Hn.double() - Href).abs()[fin].max()) < 1e-5

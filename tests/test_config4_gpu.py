@@ -1,7 +1,11 @@
 """BASELINE config-4 instance shape (n=5000, m=2500+2500, h=2048) on the GPU: exercises the
 large-instance kernel paths (24 column groups per lane, > 64 KiB dynamic LDS for the KKT / Ruiz /
-metric kernels, h = 2048 cell tiles) against the CPU oracle on one instance, T = 2.
-Same tolerances as the bench-shape test (tests/test_fullsize_gpu.py)."""
+metric kernels, h = 2048 cell tiles, the 8-column LU panels at N = 10000) against the CPU oracle
+on one instance, T = 2, and the full batch (B = 512, every offset past 2^31 elements) against
+one-instance solves bit for bit.  Same tolerances as the bench-shape test
+(tests/test_fullsize_gpu.py)."""
+import os
+
 import numpy as np
 import pytest
 import torch
@@ -11,6 +15,8 @@ from oracle import iadmm_oracle as orc
 
 pytestmark = pytest.mark.gpu
 
+N_VAR, MI, ME, H, T, LENGTH = 5000, 2500, 2500, 2048, 2, 200
+
 
 def rel_l2(a, b):
     a = torch.as_tensor(a).double().cpu()
@@ -18,22 +24,33 @@ def rel_l2(a, b):
     return float((a - b).norm() / max(b.norm(), 1e-30))
 
 
-@pytest.mark.timeout(900)  # the CPU oracle at n + m = 10000, h = 2048 alone takes minutes on a busy host
-def test_config4_shape_vs_oracle():
+@pytest.fixture(scope="module")
+def cfg4():
+    """GPU and oracle Stage-I solves of instance 0 (computed once for the tests below)."""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     from iadmm import data, solver
-    n, mi, me, h, T = 5000, 2500, 2500, 2048, 2
-    d = data.make_qp_batch(n, mi, me, 1, first_index=0, device="cuda")
-    params = data.init_lstm_params(h, 200, device="cuda")
+    d = data.make_qp_batch(N_VAR, MI, ME, 1, first_index=0, device="cuda")
+    params = data.init_lstm_params(H, LENGTH, device="cuda")
     cpu = {k: v.cpu() for k, v in d.items()}  # before the in-place scaling below
     with torch.no_grad():
-        out = solver.solve(params, d["Q"], d["p"], d["A0"], d["zl"], d["zu"], mi, me, T, 6e-6, keep_unscaled=False)
+        out = solver.solve(params, d["Q"], d["p"], d["A0"], d["zl"], d["zu"], MI, ME, T, 6e-6, keep_unscaled=False)
     torch.cuda.synchronize()
-    torch.set_num_threads(max(1, min(16, torch.get_num_threads())))
-    with torch.no_grad():
-        ref = orc.solve({k: v.cpu() for k, v in params.items()}, cpu["Q"], cpu["p"], cpu["A0"], cpu["zl"],
-                        cpu["zu"], mi, me, T, 6e-6, h)
+    threads = torch.get_num_threads()
+    torch.set_num_threads(max(1, min(16, os.cpu_count() or 1)))
+    try:
+        with torch.no_grad():
+            ref = orc.solve({k: v.cpu() for k, v in params.items()}, cpu["Q"], cpu["p"], cpu["A0"], cpu["zl"],
+                            cpu["zu"], MI, ME, T, 6e-6, H)
+    finally:
+        torch.set_num_threads(threads)
+    out = {k: out[k] for k in ("D", "x", "y", "z", "xv", "H", "C", "primal", "dual")}
+    return out, ref, cpu
+
+
+@pytest.mark.timeout(900)  # the CPU oracle at n + m = 10000, h = 2048 alone takes minutes on a busy host
+def test_config4_shape_vs_oracle(cfg4):
+    out, ref, _ = cfg4
     assert rel_l2(out["D"], torch.diagonal(ref["scaling"]["D"], dim1=1, dim2=2)) < 1e-6
     for k in ("x", "z", "xv"):
         assert rel_l2(out[k], ref[k]) < 1e-4, k
@@ -42,3 +59,99 @@ def test_config4_shape_vs_oracle():
     assert rel_l2(out["C"], ref["C"]) < 1e-4
     np.testing.assert_allclose(out["primal"].cpu().numpy(), ref["primal"].numpy(), rtol=1e-4)
     np.testing.assert_allclose(out["dual"].cpu().numpy(), ref["dual"].numpy(), rtol=1e-4)
+
+
+@pytest.mark.timeout(900)
+def test_config4_stage2_vs_oracle(cfg4):
+    """Stage II at N = n + m = 10000 (the 8-column LU panels on 1024-thread workgroups, ten panel
+    rows per thread): two exact iterations (models/lu.py) from the oracle's Stage-I end state, GPU
+    against oracle.lu_iteration (LAPACK, one thread) in fp32 and fp64.  Bound as in the config-2
+    Stage-II test (tests/test_k100_gpu.py): 1e-4, or 2x the fp32 oracle's own distance from fp64."""
+    from models.lu import LU
+    import utils
+    _, ref, cpu = cfg4
+    sigma, iters = 6e-6, 2
+    st0 = {k: ref[k].clone() for k in ("x", "y", "z", "xv", "rho_vec")}
+
+    def oracle_run(dtype):
+        st = {k: v.to(dtype) for k, v in st0.items()}
+        dd = {k: v.to(dtype) for k, v in cpu.items()}
+        K = lu = piv = None
+        traj = []
+        threads = torch.get_num_threads()
+        torch.set_num_threads(1)  # multi-threaded MKL LASWP can hang in this torch build (DESIGN.md §4)
+        try:
+            for _ in range(iters):
+                x, y, z, xv, K, _, lu, piv = orc.lu_iteration(st["rho_vec"], st["x"], st["y"], st["z"], st["xv"],
+                                                              sigma, K, lu, piv, dd["Q"], dd["p"], dd["A0"], dd["zl"],
+                                                              dd["zu"])
+                st.update(x=x, y=y, z=z, xv=xv)
+                pr, du, _ = orc.primal_dual(x, y, z, dd["Q"], dd["p"], dd["A0"])
+                traj.append(dict(x=x.double(), z=z.double(), primal=pr.reshape(-1).double(),
+                                 dual=du.reshape(-1).double()))
+        finally:
+            torch.set_num_threads(threads)
+        return traj
+
+    ref32, ref64 = oracle_run(torch.float32), oracle_run(torch.float64)
+    d = {k: v.cuda() for k, v in cpu.items()}
+    g = {k: v.cuda() for k, v in st0.items()}
+    x, y, z, xv = g["x"], g["y"], g["z"], g["xv"]
+    model = LU("cuda")
+    A_t = lu = piv = None
+    with torch.no_grad():
+        for it in range(iters):
+            x, y, z, xv, A_t, _, lu, piv = model(g["rho_vec"], x, y, z, xv, sigma, A_t, lu, piv, Q=d["Q"], p=d["p"],
+                                                 A0=d["A0"], lb=None, ub=None, zl=d["zl"], zu=d["zu"])
+            pr, du, _ = utils.primal_dual_loss(x, y, z, d["Q"], d["p"], d["A0"])
+            a = dict(x=x, z=z, primal=pr.reshape(-1), dual=du.reshape(-1))
+            msg = []
+            for k in ("x", "z", "primal", "dual"):
+                b32, b64 = ref32[it][k], ref64[it][k]
+                if k in ("x", "z"):
+                    e_gpu, e_f32 = rel_l2(a[k], b32), rel_l2(b32, b64)
+                else:
+                    e_gpu = float(((a[k].double().cpu() - b32).abs() / b32.abs().clamp_min(1e-30)).max())
+                    e_f32 = float(((b32 - b64).abs() / b64.abs().clamp_min(1e-30)).max())
+                msg.append(f"{k} {e_gpu:.2e} (fp32 oracle vs fp64 {e_f32:.2e})")
+                assert e_gpu <= max(1e-4, 2.0 * e_f32 + 1e-5), (it, k, e_gpu, e_f32)
+            print(f"[stage2 N=10000 it {it}] " + ", ".join(msg))
+
+
+B_FULL = 512
+PROBES = (0, 255, 511)
+
+
+@pytest.mark.timeout(900)
+def test_config4_full_batch_matches_single_instances():
+    """Config 4 at its real batch (B = 512: H, C and the projection partials span 1.05e10 floats,
+    so every instance past ~104 lives beyond the 2^31-element offset): instances 0, 255 and 511 of
+    the B = 512 solve (T = 2, in-place scaling) are bitwise equal to B = 1 solves of the same
+    generator indices -- every kernel on the path works per instance (instance 0's B = 1 solve is
+    the one checked against the oracle above)."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from iadmm import data, solver
+    params = data.init_lstm_params(H, LENGTH, device="cuda")
+    keys = ("x", "y", "z", "xv", "primal", "dual", "obj")
+    d = data.make_qp_batch(N_VAR, MI, ME, B_FULL, first_index=0, device="cuda")
+    with torch.no_grad():
+        out = solver.solve(params, d["Q"], d["p"], d["A0"], d["zl"], d["zu"], MI, ME, T, 6e-6, keep_unscaled=False)
+    torch.cuda.synchronize()
+    full = {i: {k: out[k][i].clone() for k in keys} for i in PROBES}
+    for i in PROBES:
+        full[i]["H_last_rows"] = out["H"][i, -64:].clone()  # the rows at the largest offsets of each instance
+        full[i]["C_last_rows"] = out["C"][i, -64:].clone()
+    assert bool(torch.isfinite(out["x"]).all())
+    del out, d
+    torch.cuda.empty_cache()
+    for i in PROBES:
+        d1 = data.make_qp_batch(N_VAR, MI, ME, 1, first_index=i, device="cuda")
+        with torch.no_grad():
+            o1 = solver.solve(params, d1["Q"], d1["p"], d1["A0"], d1["zl"], d1["zu"], MI, ME, T, 6e-6,
+                              keep_unscaled=False)
+        for k in keys:
+            assert torch.equal(o1[k][0], full[i][k]), (i, k)
+        assert torch.equal(o1["H"][0, -64:], full[i]["H_last_rows"]), i
+        assert torch.equal(o1["C"][0, -64:], full[i]["C_last_rows"]), i
+        del o1, d1

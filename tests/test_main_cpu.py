@@ -1,0 +1,31 @@
+"""Host logic of the CLI (main.py) that needs no GPU: which solver spans count as the
+reference's "Parallel Time" (main.py:825-834, 881-890, 1024-1031, 1055-1066)."""
+import os
+import re
+
+import iadmm_path  # noqa: F401
+import main
+
+from conftest import PKG
+
+# the reference times Ruiz scaling, the model() calls, the final unscale and Stage II; it does
+# not time the zero-fills of the state (allocated before start_time, main.py:836-841) or metrics
+TIMED = {"scaling", "iterations", "unscale", "stage2_factor", "stage2_iterations"}
+
+
+def _span_names():
+    names = set()
+    for fn in ("solver.py",):
+        src = open(os.path.join(PKG, "iadmm", fn)).read()
+        names |= set(re.findall(r'timer\.start\("([^"]+)"\)', src))
+    return names
+
+
+def test_timed_seconds_sums_only_the_reference_timed_spans():
+    names = _span_names()
+    assert {"scaling", "iterations", "unscale", "untimed:setup", "untimed:metrics"} <= names
+    spans = {k: 1000.0 for k in names}
+    spans.update({"k:lstm_cell": 5000.0, "hist:metrics": 7000.0})
+    counted = {k for k in spans if main.timed_seconds({k: spans[k]}) > 0}
+    assert counted == TIMED & names, counted
+    assert main.timed_seconds(spans) == len(TIMED & names)
