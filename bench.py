@@ -66,6 +66,10 @@ def parse():
     ap.add_argument("--stage2-iters", type=int, default=20,
                     help="feas_rest_num of a Stage II run (models/lu.py via main.py:1035-1066) on the solved "
                          "batch, timed and reported under 'stage2' (0: skip)")
+    ap.add_argument("--train-batch", type=int, default=512,
+                    help="instances per GPU of the training record (BASELINE config 5: 4096 over 8 GPUs; "
+                         "one warm-up + one timed TBPTT window of outer_T iterations; 0: skip)")
+    ap.add_argument("--train-micro-batch", type=int, default=128)
     ap.add_argument("--in-place-scaling", action="store_true",
                     help="scale Q/A0 in place (no unscaled copy; residuals via the scaling identity)")
     a = ap.parse_args()
@@ -208,6 +212,67 @@ def stage2_record(args, d, out, n, mi, me, B):
     return rec
 
 
+def train_record(args, d, mi, me, dist, world):
+    """BASELINE config 5 per GPU: one TBPTT window (main.py:336-358: outer_T forward iterations +
+    the residual loss + backward through all of them + gradient all-reduce + Adam step) on the
+    first ``train_batch`` instances (Ruiz-scaled copy), micro-batched; one untimed warm-up window,
+    one timed.  Per-kernel hipEvent spans of the training kernels (iadmm/autograd.TIMER) give the
+    cell backward's MFMA roofline (its recompute GEMM = the forward's 8 N h^2 flop per
+    instance-iteration, rocprof: profiles/*train*kernel_stats.csv)."""
+    from iadmm import autograd, ops, solver, train
+    from models.lstm import LSTM
+    n = args.num_var
+    N, h, T = n + mi + me, args.hidden_dim, args.outer_T
+    Bt, mb = min(args.train_batch, d["Q"].shape[0]), args.train_micro_batch
+    sc = ops.ruiz_scale(*(d[k][:Bt] for k in ("Q", "p", "A0", "zl", "zu")), 10)
+    ds = dict(zip(("Q", "p", "A0", "zl", "zu"), sc[:5]))
+    del sc
+    torch.manual_seed(17)
+    model = LSTM(mi + me, 2, h, T, "cuda")
+    opt = torch.optim.Adam(model.parameters(), lr=5e-5)  # scripts/Synthetic.sh:3
+
+    def window():
+        return train.tbptt_batch(model, ds, mi, me, T, T, args.sigma, opt, micro_batch=mb, global_batch=world * Bt,
+                                 dist=dist)
+
+    window()
+    torch.cuda.synchronize()
+    tm = solver.Timer(True)
+    autograd.TIMER = tm
+    calls0 = train.ALLREDUCE_CALLS
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    loss = window()
+    torch.cuda.synchronize()
+    el = parallel_max(time.perf_counter() - t0, dist)
+    autograd.TIMER = None
+    nb, ms_bwd = tm.stats_ms("k:cell_bwd")
+    spans = {k[2:]: v for k, v in tm.totals_ms().items()}
+    mrows = min(mb, Bt) * N                       # rows of one micro-batch launch
+    flop = 8.0 * mrows * h * h                    # recompute GEMM of one cell-backward launch
+    tf = flop / (ms_bwd * 1e-3) / 1e12
+    del ds, model, opt
+    return {"value": world * Bt / el, "unit": "training instances/s", "per_gpu": Bt / el,
+            "batch_per_gpu": Bt, "micro_batch": mb, "outer_T": T, "truncated_length": T, "ms": 1e3 * el,
+            "loss": loss, "allreduce_calls": train.ALLREDUCE_CALLS - calls0,
+            "kernel_ms_per_window": spans,
+            "roofline": {"kernel": "iadmm_lstm_cell_bwd", "bound": "mfma", "achieved": tf,
+                         "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": tf / FP32_MFMA_PEAK_TFLOPS,
+                         "avg_launch_ms": ms_bwd, "launches": nb, "algorithmic_per_launch": flop,
+                         "algorithmic": "8 N h^2 per instance-iteration (gate pre-activation recompute on MFMA); "
+                                        "the epilogue's elementwise backward is not counted"},
+            "note": "BASELINE config 5 per GPU (4096 instances over 8 GPUs = 512 each): one TBPTT window of "
+                    "main.py:336-358 (forward + loss + backward + RCCL gradient all-reduce when N > 1 + Adam), "
+                    "lr 5e-5 (scripts/Synthetic.sh:3), random init; outside the headline's timed scope"}
+
+
+def parallel_max(v, dist):
+    from iadmm import parallel
+    return parallel.max_over_ranks(v, dist, device="cuda")
+
+
 def load_weights(args, h, T):
     """(params dict on cuda, tag): the checkpoint named like main.py's (QP_{n}_{eq}_{ineq}_{T}_{h})
     under checkpoints/ for --weights auto, a given .pth, or random init."""
@@ -239,6 +304,13 @@ def launch_ranks(args):
     mod = importlib.util.module_from_spec(spec)
     spec.loader.exec_module(mod)
     mod.relaunch(os.path.abspath(sys.argv[0]), sys.argv[1:], args.gpus)
+
+
+def master_dev(d, master):
+    """Unscaled instances on the device for the training record when the solve scaled in place."""
+    if master is None:
+        return d
+    return {k: v.to("cuda") if v.device.type == "cpu" else v for k, v in master.items()}
 
 
 def heartbeat(period_s=60.0):
@@ -368,6 +440,21 @@ def main():
         rand = (prm_r, {k: out_r[k] for k in ("x", "y", "z", "primal", "dual")})
         del out_r
 
+    # BASELINE config 5 per GPU: one timed TBPTT training window (after the inference work; the
+    # solve's state is released first: the window saves ~1.6 GB of activations per iteration at
+    # micro-batch 128)
+    trn = None
+    mb_t = min(args.train_micro_batch, args.train_batch, count)
+    act_bytes = 2.0 * 4 * mb_t * N * h * T  # saved H and C of every iteration of one micro-batch
+    train_fits = act_bytes < 0.7 * torch.cuda.get_device_properties(local).total_memory
+    if args.train_batch > 0 and train_fits:
+        out_keep = {k: out[k] for k in ("x", "y", "z", "primal", "dual")}
+        out = None
+        torch.cuda.empty_cache()
+        trn = train_record(args, d if keep else master_dev(d, master), mi, me, dist, world)
+        out = out_keep
+        torch.cuda.empty_cache()
+
     res = None
     if rank == 0:
         total = world * B * args.steps
@@ -410,6 +497,11 @@ def main():
         }
         if st2 is not None:
             res["stage2"] = st2
+        if trn is not None:
+            res["train"] = trn
+        elif args.train_batch > 0:
+            res["train"] = {"skipped": f"one micro-batch of {mb_t} saves {act_bytes / 1e9:.0f} GB of activations "
+                                       "over the window (> 70 % of HBM)"}
         if alt is not None:
             res["alt_precision"] = alt
         if rand is not None:

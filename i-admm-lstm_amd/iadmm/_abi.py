@@ -39,6 +39,8 @@ SIGNATURES = {
     "iadmm_unscale": (cint, [i64, i64, i64, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp]),
     "iadmm_metrics": (cint, [i64, i64, i64, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp]),
     "iadmm_bmv": (cint, [i64, i64, i64, vp, vp, vp, cint, vp, vp]),
+    "iadmm_bmv_t": (cint, [i64, i64, i64, vp, vp, vp, vp]),
+    "iadmm_bger": (cint, [i64, i64, i64, vp, vp, cint, vp, vp]),
     "iadmm_lu_factor_ws_bytes": (i64, [i64, i64]),
     "iadmm_lu_factor": (cint, [i64, i64, vp, vp, vp, vp, i64, vp]),
     "iadmm_lu_solve": (cint, [i64, i64, vp, vp, vp, vp]),

@@ -19,6 +19,19 @@ from .solver import PARAM_NAMES
 
 GATES = "ifou"
 
+# Optional solver.Timer: hipEvent spans ("k:cell_fwd", "k:cell_bwd", "k:dH", "k:dU") around the
+# training kernels on the current stream (bench.py's training record; None = no events).
+TIMER = None
+
+
+def _span(name):
+    return TIMER.start(name) if TIMER is not None else None
+
+
+def _end(tok):
+    if tok is not None:
+        TIMER.stop(tok)
+
 
 class IterationFn(torch.autograd.Function):
     @staticmethod
@@ -36,7 +49,9 @@ class IterationFn(torch.autograd.Function):
         rho_vec = ops.empty(B, m, like=x)
         g = ops.kkt_resgrad(Q, A0, pv, x, y, z, xv, sigma, scal, num_ineq, btild=btild, rho_vec=rho_vec, r_out=r)
         Upk, Wx = packed.get({k: v.detach() for k, v in p.items()}, h)
+        k = _span("k:cell_fwd")
         Hn, Cn, part = ops.lstm_cell(H, C, xv, g, Upk, Wx)
+        _end(k)
         xvo, xo, yo, zo = ops.admm_update(n, m, num_ineq, part, det(p["b_h"]), xv, x, y, z, zl, zu, scal)
         ctx.save_for_backward(x, y, z, xv, H, C, g, r, xvo, scal, *params)
         ctx.meta = meta
@@ -60,11 +75,17 @@ class IterationFn(torch.autograd.Function):
                                                              c(dyo), c(dzo), c(dxvo))
         # 2. cell: recompute gates, dP, dC, d(in) partials, W_h slabs
         Upk, Wx = packed.get({k: v.detach() for k, v in p.items()}, h)
+        k = _span("k:cell_bwd")
         dC, dP, whslab, inpart = ops.lstm_cell_bwd(H, C, xv, g, Upk, Wx, dq, c(dHn), c(dCn))
+        _end(k)
         # 3. dH = dP U_cat^T ; [dU ; dW ; db] = [H, xv, g, 1]^T dP
         Ucat_pk = packed.get_ucat_packed({k: v.detach() for k, v in p.items()}, h)     # [h, 4h], tiled
+        k = _span("k:dH")
         dH = ops.gemm_nt_packed(dP, Ucat_pk, h).reshape(H.shape)
+        _end(k)
+        k = _span("k:dU")
         dUcat = ops.gemm_tn(H.reshape(M, h), dP)
+        _end(k)
         X3 = torch.stack([xv.reshape(M), g.reshape(M), torch.ones(M, device=x.device)], dim=1).contiguous()
         dW3 = ops.gemm_tn(X3, dP, rows_per_split=512)                                 # [3, 4h], streaming
         dWh = ops.slab_reduce(whslab).reshape(h, 1)
@@ -89,24 +110,130 @@ class IterationFn(torch.autograd.Function):
 
 
 class LossFn(torch.autograd.Function):
-    """(||A0 x - z||, ||Q x + p + A0^T y||) per instance (utils.py:68-71); the data (Q, p, A0) is
-    constant (no gradient)."""
+    """(||A0 x - z||, ||Q x + p + A0^T y||) per instance (utils.py:68-71).  x, y, z: the training
+    loss's inputs (iadmm_loss_grad_split sweeps); Q, p, A0: data, differentiable too when they
+    require grad (rank-1 iadmm_bger terms from the two residual vectors)."""
 
     @staticmethod
-    def forward(ctx, x, y, z, data):
-        Q, pv, A0 = data
+    def forward(ctx, x, y, z, Q, pv, A0):
         # one sweep (row-block split: fills the chip at the micro-batch); the gradient sweep runs in
         # backward
         pr, du, _, _, _ = ops.loss_grad(Q, pv, A0, x, y, z, want_grad=False)
-        ctx.save_for_backward(x, y, z)
-        ctx.data = data
+        ctx.save_for_backward(x, y, z, Q, pv, A0, pr, du)
         return pr, du
 
     @staticmethod
     def backward(ctx, dpr, ddu):
-        x, y, z = ctx.saved_tensors
-        Q, pv, A0 = ctx.data
+        x, y, z, Q, pv, A0, pr, du = ctx.saved_tensors
         cp = dpr.contiguous() if dpr is not None else torch.zeros(x.shape[0], device=x.device)
         cd = ddu.contiguous() if ddu is not None else torch.zeros(x.shape[0], device=x.device)
-        _, _, dx, dy, dz = ops.loss_grad(Q, pv, A0, x, y, z, cp, cd)
-        return dx, dy, dz, None
+        dx = dy = dz = dQ = dp = dA = None
+        if any(ctx.needs_input_grad[:3]):
+            _, _, dx, dy, dz = ops.loss_grad(Q, pv, A0, x, y, z, cp, cd)
+        if any(ctx.needs_input_grad[3:]):
+            # unit residual directions scaled by the upstream coefficients (norm' = r / ||r||; a
+            # zero residual gives 0 like torch's vector_norm backward)
+            r = ops.bmv(A0, x) - z
+            d = ops.bmv(Q, x) + pv + ops.bmv_t(A0, y)
+            wr = (r * (cp / pr).nan_to_num(0.0, 0.0, 0.0).reshape(-1, 1)).contiguous()
+            wd = (d * (cd / du).nan_to_num(0.0, 0.0, 0.0).reshape(-1, 1)).contiguous()
+            if ctx.needs_input_grad[3]:
+                dQ = ops.bger(wd, x)
+            if ctx.needs_input_grad[4]:
+                dp = wd
+            if ctx.needs_input_grad[5]:
+                dA = ops.bger(wr, x)
+                ops.bger(y, wd, out=dA, accumulate=True)
+        return dx, dy, dz, dQ, dp, dA
+
+
+# ----------------------------------------------------------------------------- reporting metrics
+# utils.py:53-60 are plain torch expressions in the reference, so autograd reaches x and the data.
+# Their backward here: the matvecs on iadmm_bmv / iadmm_bmv_t, the matrix gradients (rank 1 per
+# instance) on iadmm_bger; the [B, rows] vector algebra in between is elementwise.  The gradient
+# conventions are torch's: clamp(min=0) passes where its input >= 0, abs' derivative is sgn (0 at 0).
+
+def _vec(a):
+    return a.reshape(a.shape[0], -1).contiguous()
+
+
+class ObjFn(torch.autograd.Function):
+    """0.5 x^T Q x + p^T x per instance (utils.py:53-54): x [B,n], Q [B,n,n], p [B,n] -> [B]."""
+
+    @staticmethod
+    def forward(ctx, x, Q, p):
+        B, n = x.shape
+        zeros = x.new_zeros(B, 0)
+        obj, _, _ = ops.metrics(Q, p, Q.new_zeros(B, 0, n), x, zeros, zeros)
+        ctx.save_for_backward(x, Q, p)
+        return obj
+
+    @staticmethod
+    def backward(ctx, g):
+        x, Q, p = ctx.saved_tensors
+        g = g.reshape(-1, 1).contiguous()
+        hx = (0.5 * g) * x                   # d/d(Qx) of 0.5 x^T (Qx)
+        dx = dQ = dp = None
+        if ctx.needs_input_grad[0]:
+            dx = ops.bmv(Q, x) * (0.5 * g) + ops.bmv_t(Q, hx.contiguous()) + g * p
+        if ctx.needs_input_grad[1]:
+            dQ = ops.bger(hx.contiguous(), x)
+        if ctx.needs_input_grad[2]:
+            dp = g * x
+        return dx, dQ, dp
+
+
+class IneqDistFn(torch.autograd.Function):
+    """clamp(G x - c, 0) (utils.py:56-57): x [B,n], G [B,mi,n], c [B,mi] -> [B,mi]."""
+
+    @staticmethod
+    def forward(ctx, x, G, c):
+        pre = ops.bmv(G, x) - c
+        ctx.save_for_backward(x, G, pre >= 0)
+        return torch.clamp(pre, min=0)
+
+    @staticmethod
+    def backward(ctx, w):
+        x, G, mask = ctx.saved_tensors
+        w = (w * mask).contiguous()
+        dx = ops.bmv_t(G, w) if ctx.needs_input_grad[0] else None
+        dG = ops.bger(w, x) if ctx.needs_input_grad[1] else None
+        dc = -w if ctx.needs_input_grad[2] else None
+        return dx, dG, dc
+
+
+class EqDistFn(torch.autograd.Function):
+    """|b - A x| (utils.py:59-60): x [B,n], A [B,me,n], b [B,me] -> [B,me]."""
+
+    @staticmethod
+    def forward(ctx, x, A, b):
+        r = b - ops.bmv(A, x)
+        ctx.save_for_backward(x, A, torch.sgn(r))
+        return r.abs()
+
+    @staticmethod
+    def backward(ctx, w):
+        x, A, s = ctx.saved_tensors
+        ws = (w * s).contiguous()               # d/dr
+        dx = -ops.bmv_t(A, ws) if ctx.needs_input_grad[0] else None
+        dA = -ops.bger(ws, x) if ctx.needs_input_grad[1] else None
+        db = ws if ctx.needs_input_grad[2] else None
+        return dx, dA, db
+
+
+class BmvFn(torch.autograd.Function):
+    """Differentiable batched matvec M x (M [B,R,C], x [B,C] -> [B,R]): iadmm_bmv forward,
+    iadmm_bmv_t / iadmm_bger backward.  The building block of utils.aug_lagr under grad."""
+
+    @staticmethod
+    def forward(ctx, M, x):
+        ctx.save_for_backward(M, x)
+        return ops.bmv(M, x)
+
+    @staticmethod
+    def backward(ctx, g):
+        M, x = ctx.saved_tensors
+        g = g.contiguous()
+        dM = ops.bger(g, x) if ctx.needs_input_grad[0] else None
+        dx = ops.bmv_t(M, g) if ctx.needs_input_grad[1] else None
+        return dM, dx

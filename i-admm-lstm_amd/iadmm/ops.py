@@ -218,6 +218,24 @@ def bmv(Mx, x, rhs=None, mode=BMV_PLAIN):
     return out
 
 
+def bmv_t(Mx, v, out=None):
+    """Batched transposed matvec Mx^T v: Mx [B,R,C], v [B,R] -> [B,C]."""
+    B, R, C = Mx.shape
+    out = empty(B, C, like=Mx) if out is None else out
+    _abi.call("iadmm_bmv_t", B, R, C, _p(Mx), _p(v), _p(out), _stream())
+    return out
+
+
+def bger(u, v, out=None, accumulate=False):
+    """Per-instance rank-1 product u v^T: u [B,R], v [B,C] -> [B,R,C] (added to ``out`` with
+    ``accumulate``)."""
+    B, R = u.shape
+    C = v.shape[1]
+    out = empty(B, R, C, like=u) if out is None else out
+    _abi.call("iadmm_bger", B, R, C, _p(u), _p(v), int(bool(accumulate)), _p(out), _stream())
+    return out
+
+
 def kkt_matvec(Q, A0, v, sigma, scal, num_ineq, transpose=False, rho_rows=None):
     """Implicit K v or K^T v, v[B,n+m] -> [B,n+m]."""
     B, n = Q.shape[0], Q.shape[1]

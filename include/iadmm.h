@@ -213,6 +213,14 @@ int iadmm_metrics(int64_t B, int64_t n, int64_t m, const float* Q, const float* 
 int iadmm_bmv(int64_t B, int64_t R, int64_t C, const float* M, const float* x, const float* rhs,
               int mode, float* out, void* stream);
 
+/* Backward primitives of the reporting metrics (utils.py:53-60 obj_fn / ineq_dist / eq_dist under
+ * autograd; iadmm/autograd.py ObjFn, IneqDistFn, EqDistFn):
+ *   iadmm_bmv_t: out[B,C] = M[B,R,C]^T v[B,R] (fixed-order sums over r; R floats of LDS <= 160 KiB)
+ *   iadmm_bger:  out[B,R,C] = (accumulate ? out : 0) + u[B,R] v[B,C]^T (per-instance rank 1) */
+int iadmm_bmv_t(int64_t B, int64_t R, int64_t C, const float* M, const float* v, float* out, void* stream);
+int iadmm_bger(int64_t B, int64_t R, int64_t C, const float* u, const float* v, int accumulate, float* out,
+               void* stream);
+
 /* ------------------------------------------------------------------------------------------
  * Training backward (autograd through models/lstm.py:47-96 and utils.py:68-71; main.py:336-358).
  * All reductions are fixed-order partial slabs: gradients are bitwise reproducible.

@@ -14,7 +14,8 @@ Reference anchors (``/root/reference``):
   * ``models/lstm.py:47-96``  one Stage-I iteration  -> :func:`lstm_iteration`
   * ``models/lu.py:13-47``    one Stage-II iteration -> :func:`lu_iteration`
   * ``methods/scaling.py:17-119`` modified Ruiz     -> :func:`ruiz`
-  * ``utils.py:53-71``        metrics               -> :func:`primal_dual`, :func:`objective`
+  * ``utils.py:53-78``        metrics               -> :func:`primal_dual`, :func:`objective`,
+                                                       :func:`ineq_dist`, :func:`eq_dist`, :func:`aug_lagr`
   * ``main.py:818-1031``      test-mode solve loop  -> :func:`solve`
 """
 from __future__ import annotations
@@ -161,6 +162,25 @@ def ruiz(Q, p, A0, zl, zu, iters=10):
 def objective(x, Q, p):
     """utils.py:53-54."""
     return 0.5 * torch.bmm(x.permute(0, 2, 1), torch.bmm(Q, x)) + torch.bmm(p.permute(0, 2, 1), x)
+
+
+def ineq_dist(x, G, c):
+    """utils.py:56-57."""
+    return torch.clamp(torch.bmm(G, x) - c, 0)
+
+
+def eq_dist(x, A, b):
+    """utils.py:59-60."""
+    return torch.abs(b - torch.bmm(A, x))
+
+
+def aug_lagr(x, z, y, Q, p, A0, rho_vec):
+    """utils.py:74-78 (with its Q p term)."""
+    r = torch.bmm(A0, x) - z
+    fx = 0.5 * torch.bmm(x.permute(0, 2, 1), torch.bmm(Q, p)) + torch.bmm(p.permute(0, 2, 1), x)
+    dual_item = torch.bmm(y.permute(0, 2, 1), r)
+    aug_item = 0.5 * torch.bmm(r.permute(0, 2, 1), torch.bmm(torch.diag_embed(rho_vec.squeeze(-1)), r))
+    return fx + dual_item + aug_item
 
 
 def primal_dual(x, y, z, Q, p, A0):

@@ -66,6 +66,10 @@ def test_bench_single_gpu_contract():
     assert par["x_rel_l2"] <= par["tol"]["x"] and par["primal_max_rel"] <= par["tol"]["primal"]
     # the GPU and the CPU oracle solved the same instances: residuals of the same magnitude
     assert r["final_residual"]["primal_mean"] > 0
+    # config-5 training record: one timed TBPTT window, cell-backward roofline
+    tr = r["train"]
+    assert tr["value"] > 0 and tr["loss"] == tr["loss"] and tr["batch_per_gpu"] == 8
+    assert tr["roofline"]["launches"] == 3 and tr["roofline"]["bound"] == "mfma"
 
 
 def test_bench_two_ranks_shared_gpu():

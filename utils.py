@@ -56,29 +56,43 @@ def _flat(a):
     return a.detach().float().reshape(a.shape[0], -1).contiguous()
 
 
-def _no_grad_inputs(*ts):
-    if torch.is_grad_enabled() and any(isinstance(t, torch.Tensor) and t.requires_grad for t in ts):
-        raise NotImplementedError("metric backward kernels are not built yet; use torch.no_grad()")
+def _wants_grad(*ts):
+    return torch.is_grad_enabled() and any(isinstance(t, torch.Tensor) and t.requires_grad for t in ts)
+
+
+def _f32(a):
+    """fp32 contiguous view that keeps the autograd graph (the Functions below get differentiable
+    inputs; their backward kernels compute in fp32 like the forward)."""
+    return a.float().contiguous()
 
 
 def obj_fn(x, Q, p):
-    """1/2 x^T Q x + p^T x, [B,1,1] (utils.py:53-54)."""
-    _no_grad_inputs(x, Q, p)
+    """1/2 x^T Q x + p^T x, [B,1,1] (utils.py:53-54).  Differentiable in x, Q, p
+    (iadmm.autograd.ObjFn: backward on iadmm_bmv / iadmm_bmv_t / iadmm_bger)."""
     B, n = x.shape[0], x.shape[1]
+    if _wants_grad(x, Q, p):
+        from iadmm.autograd import ObjFn
+        return ObjFn.apply(_f32(x.reshape(B, n)), _f32(Q), _f32(p.reshape(B, n))).reshape(B, 1, 1)
     zeros = x.new_zeros(B, 0)
     obj, _, _ = ops.metrics(Q.detach().float().contiguous(), _flat(p), Q.new_zeros(B, 0, n), _flat(x), zeros, zeros)
     return obj.reshape(B, 1, 1)
 
 
 def ineq_dist(x, G, c):
-    """max(G x - c, 0), [B,mi,1] (utils.py:56-57)."""
-    _no_grad_inputs(x, G, c)
+    """max(G x - c, 0), [B,mi,1] (utils.py:56-57).  Differentiable in x, G, c (IneqDistFn)."""
+    if _wants_grad(x, G, c):
+        from iadmm.autograd import IneqDistFn
+        B = x.shape[0]
+        return IneqDistFn.apply(_f32(x.reshape(B, -1)), _f32(G), _f32(c.reshape(B, -1))).unsqueeze(-1)
     return ops.bmv(G.detach().float().contiguous(), _flat(x), _flat(c), ops.BMV_POS_EXCESS).unsqueeze(-1)
 
 
 def eq_dist(x, A, b):
-    """|b - A x|, [B,me,1] (utils.py:59-60)."""
-    _no_grad_inputs(x, A, b)
+    """|b - A x|, [B,me,1] (utils.py:59-60).  Differentiable in x, A, b (EqDistFn)."""
+    if _wants_grad(x, A, b):
+        from iadmm.autograd import EqDistFn
+        B = x.shape[0]
+        return EqDistFn.apply(_f32(x.reshape(B, -1)), _f32(A), _f32(b.reshape(B, -1))).unsqueeze(-1)
     return ops.bmv(A.detach().float().contiguous(), _flat(x), _flat(b), ops.BMV_ABS_GAP).unsqueeze(-1)
 
 
@@ -94,18 +108,14 @@ def ub_dist(x, ub):
 
 def primal_dual_loss(x, y, z, Q, p, A0):
     """(||A0 x - z||, ||Q x + p + A0^T y||, sum), each [B,1,1] (utils.py:68-71).  Differentiable
-    in x, y, z (the training loss, main.py:346) through iadmm.autograd.LossFn."""
+    in x, y, z (the training loss, main.py:346) and in the data through iadmm.autograd.LossFn."""
     B = x.shape[0]
-    if torch.is_grad_enabled() and any(t.requires_grad for t in (x, y, z)):
+    if _wants_grad(x, y, z, Q, p, A0):
         from iadmm.autograd import LossFn
-        _no_grad_inputs(Q, p, A0)
-        data = (Q.detach().float().contiguous(), p.detach().float().reshape(B, -1).contiguous(),
-                A0.detach().float().contiguous())
-        pr, du = LossFn.apply(x.float().reshape(B, -1).contiguous(), y.float().reshape(B, -1).contiguous(),
-                              z.float().reshape(B, -1).contiguous(), data)
+        pr, du = LossFn.apply(_f32(x.reshape(B, -1)), _f32(y.reshape(B, -1)), _f32(z.reshape(B, -1)), _f32(Q),
+                              _f32(p.reshape(B, -1)), _f32(A0))
         pr, du = pr.reshape(B, 1, 1), du.reshape(B, 1, 1)
         return pr, du, pr + du
-    _no_grad_inputs(x, y, z, Q, p, A0)
     _, pr, du = ops.metrics(Q.detach().float().contiguous(), _flat(p), A0.detach().float().contiguous(),
                             _flat(x), _flat(y), _flat(z))
     pr, du = pr.reshape(B, 1, 1), du.reshape(B, 1, 1)
@@ -114,12 +124,19 @@ def primal_dual_loss(x, y, z, Q, p, A0):
 
 def aug_lagr(x, z, y, Q, p, A0, rho_vec):
     """utils.py:74-78, including the reference's ``Q p`` (not ``Q x``) in the quadratic term;
-    only used by commented-out analysis code in the reference."""
-    _no_grad_inputs(x, z, y, Q, p, A0, rho_vec)
-    Qf, Af = Q.detach().float().contiguous(), A0.detach().float().contiguous()
-    Qp = ops.bmv(Qf, _flat(p))
-    r = ops.bmv(Af, _flat(x)) - _flat(z)
-    fx = 0.5 * (_flat(x) * Qp).sum(1) + (_flat(p) * _flat(x)).sum(1)
-    dual_item = (_flat(y) * r).sum(1)
-    aug_item = 0.5 * (r * (_flat(rho_vec) * r)).sum(1)
+    only used by commented-out analysis code in the reference.  Under grad the two matvecs run as
+    iadmm.autograd.BmvFn (HIP forward and backward) and the rest is elementwise."""
+    B = x.shape[0]
+    if _wants_grad(x, z, y, Q, p, A0, rho_vec):
+        from iadmm.autograd import BmvFn
+        xf, zf, yf, pf, rf = (_f32(t.reshape(B, -1)) for t in (x, z, y, p, rho_vec))
+        Qp = BmvFn.apply(_f32(Q), pf)
+        r = BmvFn.apply(_f32(A0), xf) - zf
+    else:
+        xf, zf, yf, pf, rf = (_flat(t) for t in (x, z, y, p, rho_vec))
+        Qp = ops.bmv(Q.detach().float().contiguous(), pf)
+        r = ops.bmv(A0.detach().float().contiguous(), xf) - zf
+    fx = 0.5 * (xf * Qp).sum(1) + (pf * xf).sum(1)
+    dual_item = (yf * r).sum(1)
+    aug_item = 0.5 * (r * (rf * r)).sum(1)
     return (fx + dual_item + aug_item).reshape(-1, 1, 1)
