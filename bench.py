@@ -103,6 +103,27 @@ def pmc_traffic(kernel_prefix, n, m, h, B, lanes=1):
     return tot
 
 
+def pmc_traffic_stage2(n, m, B):
+    """HBM bytes of one factorization (every lu_* kernel but the solve) from the committed Stage-II
+    PMC summaries of tools/profile_lu.py (one factorization; tools/pmc_summary.py: per-kernel mean
+    per dispatch x dispatches), FETCH_SIZE x 2
+    (gfx950 correction) + WRITE_SIZE; None without a matching profile."""
+    import csv
+    import glob
+    tot = 0.0
+    for ctr, mult in (("FETCH_SIZE", 2.0), ("WRITE_SIZE", 1.0)):
+        files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_stage2_pmc_{ctr}_N{n + m}_B{B}.csv")))
+        if not files:
+            return None
+        rows = [r for r in csv.DictReader(open(files[-1]))
+                if "iadmm::lu_" in r["kernel"] and "solve" not in r["kernel"] and r["counter"] == ctr]
+        if not rows:
+            return None
+        # the profile run factors once (tools/profile_lu.py): every dispatch belongs to it
+        tot += mult * sum(float(r["mean"]) * float(r["dispatches"]) for r in rows) * 1024.0
+    return tot
+
+
 def baseline_config(args, world):
     shape = (args.num_var, args.num_ineq, args.num_eq, args.hidden_dim, args.outer_T, args.batch)
     if shape == (1000, 500, 500, 800, 100, 1024):
@@ -202,8 +223,19 @@ def stage2_record(args, d, out, n, mi, me, B):
     spans = tm.totals_ms()
     from iadmm import ops
     pr = ops.metrics(d["Q"], d["p"].reshape(B, n), d["A0"], r["x"], r["y"], r["z"])
+    N = n + mi + me
+    fac_ms = spans.get("stage2_factor")
+    fac_flop = B * 2.0 / 3.0 * N ** 3
+    fac_tf = fac_flop / (fac_ms * 1e-3) / 1e12
     rec = {"value": B / el, "unit": "QP instances/s", "feas_rest_num": args.stage2_iters, "ms": 1e3 * el,
-           "factor_ms": spans.get("stage2_factor"), "solve_iter_ms": spans.get("stage2_iterations", 0.0) / args.stage2_iters,
+           "assemble_ms": spans.get("stage2_assemble"), "factor_ms": fac_ms,
+           "solve_iter_ms": spans.get("stage2_iterations", 0.0) / args.stage2_iters,
+           "roofline": {"kernel": "iadmm_lu_factor", "bound": "mfma", "achieved": fac_tf,
+                        "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": fac_tf / FP32_MFMA_PEAK_TFLOPS,
+                        "algorithmic_per_launch": fac_flop, "algorithmic": "2/3 N^3 per instance (getrf)",
+                        "traffic": pmc_traffic_stage2(n, mi + me, B),
+                        "traffic_source": "profiles/r*_stage2_pmc_{FETCH,WRITE}_SIZE_N*_B*.csv, all LU kernels "
+                                          "of one factorization (separate --pmc passes)"},
            "chunk": r["chunk"], "final_primal_mean": float(pr[1].mean()), "final_dual_mean": float(pr[2].mean()),
            "note": "Stage II (--feas_rest) on the solved batch: K assembled from the last Stage-I rho on the "
                    "unscaled data, batched blocked LU (csrc/lu.hip) once, feas_rest_num solves + alpha=1.6 "

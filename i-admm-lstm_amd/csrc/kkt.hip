@@ -601,6 +601,88 @@ __global__ __launch_bounds__(256) void kkt_assemble_kernel(int n, int m, int num
   }
 }
 
+// Row-band form (n % 4 == 0, m % 4 == 0, 16-B aligned Q, A0, K): a workgroup writes 32 whole rows
+// of K with 16-B stores.  Top rows i < n: [Q_i + sigma e_i | column i of A0], the A0^T part staged
+// through LDS 256 constraint rows at a time (A0[j][i0 .. i0+32) read as 128-B row pieces, written
+// back as 1-KiB runs of K's row); bottom rows: [A0_{i-n} | -1/rho on the diagonal, 0 elsewhere].
+constexpr int kAsmRows = 32;
+constexpr int kAsmJ = 256;
+__global__ __launch_bounds__(256) void kkt_assemble_rows_kernel(int n, int m, int num_ineq, const float* Q,
+                                                                const float* A0, float sigma, const float* scal,
+                                                                const float* rho_rows, float* K) {
+  __shared__ float T[kAsmJ][kAsmRows + 1];
+  const int N = n + m;
+  const size_t b = blockIdx.x;
+  const int i0 = blockIdx.y * kAsmRows;
+  const int tid = threadIdx.x;
+  const float* Qb = Q + b * (size_t)n * n;
+  const float* Ab = A0 + b * (size_t)m * n;
+  float* Kb = K + b * (size_t)N * N;
+  const int nr = min(kAsmRows, N - i0);
+  const float irho_in = scal ? scal[IADMM_S_IRHO_IN] : 0.f, irho_eq = scal ? scal[IADMM_S_IRHO_EQ] : 0.f;
+  // left block columns [0, n): Q rows (+ sigma on the diagonal) or A0 rows
+  const int q4 = n >> 2;
+  for (int idx = tid; idx < nr * q4; idx += blockDim.x) {
+    const int r = idx / q4, c = (idx - r * q4) * 4, i = i0 + r;
+    float4 v;
+    if (i < n) {
+      v = *reinterpret_cast<const float4*>(Qb + (size_t)i * n + c);
+      if (i >= c && i < c + 4) {
+        if (i == c) v.x += sigma; else if (i == c + 1) v.y += sigma; else if (i == c + 2) v.z += sigma; else v.w += sigma;
+      }
+    } else {
+      v = *reinterpret_cast<const float4*>(Ab + (size_t)(i - n) * n + c);
+    }
+    *reinterpret_cast<float4*>(Kb + (size_t)i * N + c) = v;
+  }
+  if (m == 0) return;
+  const int m4 = m >> 2;
+  if (i0 >= n) {  // bottom rows: -1/rho on the diagonal of the right block
+    for (int idx = tid; idx < nr * m4; idx += blockDim.x) {
+      const int r = idx / m4, c = (idx - r * m4) * 4, i = i0 + r, d = i - n;
+      float4 v = make_float4(-0.f, -0.f, -0.f, -0.f);
+      if (d >= c && d < c + 4) {
+        const float val = rho_rows ? -(1.0f / rho_rows[b * m + d]) : -(d < num_ineq ? irho_in : irho_eq);
+        if (d == c) v.x = val; else if (d == c + 1) v.y = val; else if (d == c + 2) v.z = val; else v.w = val;
+      }
+      *reinterpret_cast<float4*>(Kb + (size_t)i * N + n + c) = v;
+    }
+    return;
+  }
+  // top rows (i0 + nr <= n since n % 32 is not assumed: rows past n in this band take the bottom
+  // form below): the A0^T block through LDS
+  const int ntop = min(nr, n - i0);
+  for (int j0 = 0; j0 < m; j0 += kAsmJ) {
+    const int nj = min(kAsmJ, m - j0);
+    __syncthreads();
+    for (int idx = tid; idx < nj * (kAsmRows / 4); idx += blockDim.x) {
+      const int jj = idx >> 3, c = (idx & 7) * 4;
+      if (c < ntop) {
+        const float* src = Ab + (size_t)(j0 + jj) * n + i0 + c;
+        const float4 v = *reinterpret_cast<const float4*>(src);  // n % 4 == 0, i0 + c % 4 == 0
+        T[jj][c] = v.x; T[jj][c + 1] = v.y; T[jj][c + 2] = v.z; T[jj][c + 3] = v.w;
+      }
+    }
+    __syncthreads();
+    const int nj4 = nj >> 2;
+    for (int idx = tid; idx < ntop * nj4; idx += blockDim.x) {
+      const int r = idx / nj4, q = (idx - r * nj4) * 4;
+      *reinterpret_cast<float4*>(Kb + (size_t)(i0 + r) * N + n + j0 + q) =
+          make_float4(T[q][r], T[q + 1][r], T[q + 2][r], T[q + 3][r]);
+    }
+  }
+  // rows of this band at or past n (when n % 32 != 0): the bottom form
+  for (int idx = tid; idx < (nr - ntop) * m4; idx += blockDim.x) {
+    const int r = ntop + idx / m4, c = (idx % m4) * 4, i = i0 + r, d = i - n;
+    float4 v = make_float4(-0.f, -0.f, -0.f, -0.f);
+    if (d >= c && d < c + 4) {
+      const float val = rho_rows ? -(1.0f / rho_rows[b * m + d]) : -(d < num_ineq ? irho_in : irho_eq);
+      if (d == c) v.x = val; else if (d == c + 1) v.y = val; else if (d == c + 2) v.z = val; else v.w = val;
+    }
+    *reinterpret_cast<float4*>(Kb + (size_t)i * N + n + c) = v;
+  }
+}
+
 inline bool kkt_fits(int64_t n, int64_t m) { return 3 * n + 2 * m <= 40960; }
 
 template <int NG, bool VEC, bool PASS2, int NT>
@@ -855,6 +937,14 @@ extern "C" int iadmm_kkt_assemble(int64_t B, int64_t n, int64_t m, int64_t num_i
   if (B <= 0 || n <= 0 || m < 0 || num_ineq < 0 || num_ineq > m || !Q || !K || (m > 0 && !A0))
     return IADMM_E_ARG;
   if (m > 0 && !scal && !rho_rows) return IADMM_E_ARG;
+  if (n % 4 == 0 && m % 4 == 0 && aligned16(Q) && aligned16(K) && (m == 0 || aligned16(A0))) {
+    const int64_t nb = (n + m + kAsmRows - 1) / kAsmRows;
+    if (B > 0x7fffffff || nb > 65535) return IADMM_E_SIZE;
+    hipLaunchKernelGGL(kkt_assemble_rows_kernel, dim3((unsigned)B, (unsigned)nb), dim3(256), 0, (hipStream_t)stream,
+                       (int)n, (int)m, (int)num_ineq, Q, A0, sigma, scal, rho_rows, K);
+    IADMM_CHECK_LAUNCH();
+    return 0;
+  }
   const int64_t ntile = (n + m + kAsmT - 1) / kAsmT;
   if (B > 0x7fffffff || ntile * ntile > 65535) return IADMM_E_SIZE;
   hipLaunchKernelGGL(kkt_assemble_kernel, dim3((unsigned)B, (unsigned)(ntile * ntile)), dim3(256), 0,

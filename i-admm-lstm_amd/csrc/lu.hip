@@ -318,20 +318,21 @@ __global__ __launch_bounds__(64) void lu_block_perm_kernel(int N, int K0, int ce
 }
 
 // Once per block: its row interchanges on the columns outside it (the final L left of it, A12 /
-// A22 right of it), and for the right columns U12 = L11^-1 A12 on the block rows (L11 = the
+// A22 right of it), and for the right columns [cend, trsm_end) U12 = L11^-1 A12 on the block rows (L11 = the
 // block's unit-lower multipliers, in LDS, broadcast reads).  One thread per column.  Every row
 // outside the block that the interchanges touch ends up holding an original block row, so: the
 // new block rows are loaded first (x, registers), then the outside rows are moved 16 at a time
 // (their sources are block rows, which are only stored to afterwards), then the substitution and
 // the block-row stores.  Column index space: [0, K0) then [cend, N).
-__global__ __launch_bounds__(256) void lu_swap_trsm_block_kernel(int N, int K0, int cend, float* A, const int* perm) {
+__global__ __launch_bounds__(256) void lu_swap_trsm_block_kernel(int N, int K0, int cend, int trsm_end, float* A,
+                                                                 const int* perm) {
   __shared__ float Ld[kBlk][kBlk + 1];
   __shared__ int prow[2 * kBlk], pcur[2 * kBlk], pcnt[1];
   const int tid = threadIdx.x;
   const size_t b = blockIdx.x;
   float* Ab = A + b * (size_t)N * N;
   const int nbk = cend - K0;
-  if (cend < N)
+  if (trsm_end > cend)
     for (int idx = tid; idx < kBlk * kBlk; idx += blockDim.x) {
       const int r = idx / kBlk, c = idx % kBlk;
       Ld[r][c] = Ab[(size_t)(K0 + r) * N + K0 + c];
@@ -355,7 +356,7 @@ __global__ __launch_bounds__(256) void lu_swap_trsm_block_kernel(int N, int K0, 
     for (int i = 0; i < 16; ++i)
       if (i0 + i < cnt) Ab[(size_t)prow[i0 + i] * N + c] = y[i];
   }
-  if (c >= cend) {  // right of the block: nbk == kBlk
+  if (c >= cend && c < trsm_end) {  // right of the block (nbk == kBlk): U12 = L11^-1 A12 where asked
 #pragma unroll
     for (int i = 1; i < kBlk; ++i) {
       float s = x[i];
@@ -369,7 +370,8 @@ __global__ __launch_bounds__(256) void lu_swap_trsm_block_kernel(int N, int K0, 
     if (i < nbk) Ab[(size_t)(K0 + i) * N + c] = x[i];
 }
 
-// A22 -= L21 U12 (rank 64) on the trailing matrix [c0, N)^2, c0 = K0 + 64.  A workgroup (8 waves,
+// A22 -= L21 U12 (rank 64) on the trailing matrix [c0, N) x [c0, cmax), c0 = K0 + 64 (cmax = N, or
+// K0 + 128 for the second half of a 128-column block: the "mid" update of lu_factor_blocks).  A workgroup (8 waves,
 // one per CU) owns a 128-column strip [cb, cb + 128) over kTRW rows [rs, re): U12's 64 x 128
 // block is staged once, transposed, in LDS (Ut); the rows are streamed in steps of 64 with a
 // one-step software pipeline.  A22 moves between HBM and the accumulators through LDS (Cin /
@@ -382,7 +384,8 @@ __global__ __launch_bounds__(256) void lu_swap_trsm_block_kernel(int N, int K0, 
 // of the 16 strips).  VEC: N % 4 == 0 and 16-B aligned rows (16-B global accesses).
 // DIAG (tools/lubench.hip only): 1 = no MFMAs (the memory pipeline alone).
 template <bool VEC, int DIAG = 0>
-__global__ __launch_bounds__(kTrailThreads, 1) void lu_trail_kernel(int N, int K0, int ntc, int nrc, float* A) {
+__global__ __launch_bounds__(kTrailThreads, 1) void lu_trail_kernel(int N, int K0, int ntc, int nrc, int cmax,
+                                                                      float* A) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   float* Ut = sm;                       // [kTC cols][kTS]: U12^T
   float* Lsb = Ut + kTC * kTS;          // 2 x [kTRS rows][kTS]: -L21
@@ -426,7 +429,7 @@ __global__ __launch_bounds__(kTrailThreads, 1) void lu_trail_kernel(int N, int K
 #pragma unroll
     for (int q = 0; q < kCQ; ++q) {
       const int e = tid + NT * q, row = rs + step * kTRS + e / CPR, col = cb + (e % CPR) * W;
-      c[q] = ld(min(row, re - 1), min(col, N - W), row < re && col < N);
+      c[q] = ld(min(row, re - 1), min(col, N - W), row < re && col < cmax);
     }
   };
   auto loadL = [&](int step, VT (&l)[kLQ]) {
@@ -454,7 +457,7 @@ __global__ __launch_bounds__(kTrailThreads, 1) void lu_trail_kernel(int N, int K
 #pragma unroll
     for (int q = 0; q < kCQ; ++q) {
       const int e = tid + NT * q, row = rs + step * kTRS + e / CPR, col = cb + (e % CPR) * W;
-      if (row < re && col < N) {
+      if (row < re && col < cmax) {
         const float* s = Cout + (e / CPR) * kCS + (e % CPR) * W;
         if constexpr (VEC) *reinterpret_cast<float4*>(Ab + (size_t)row * N + col) = *reinterpret_cast<const float4*>(s);
         else Ab[(size_t)row * N + col] = *s;
@@ -477,7 +480,7 @@ __global__ __launch_bounds__(kTrailThreads, 1) void lu_trail_kernel(int N, int K
 #pragma unroll
   for (int q = 0; q < kUQ; ++q) {  // U12 block -> Ut (transposed)
     const int e = tid + NT * q, k = e / CPR, cl = (e % CPR) * W, col = cb + cl;
-    const VT u = ld(K0 + k, min(col, N - W), col < N);
+    const VT u = ld(K0 + k, min(col, N - W), col < cmax);
     if constexpr (VEC) {
       Ut[(cl + 0) * kTS + k] = u.x; Ut[(cl + 1) * kTS + k] = u.y;
       Ut[(cl + 2) * kTS + k] = u.z; Ut[(cl + 3) * kTS + k] = u.w;
@@ -516,6 +519,227 @@ __global__ __launch_bounds__(kTrailThreads, 1) void lu_trail_kernel(int N, int K
     storeOut(step);
     __syncthreads();  // Cout drained, Cin / Ls hold the next step
     if (more) accFromCin(acc);
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// 128-column outer blocks (r03).  The rank-64 update streams A22 through HBM once per 64 columns at
+// 16 flop/B, under the fp32 MFMA ridge; per 128-column block [P, P + 128) the two 64-column halves
+// are factored one after the other (the second half updated by the first: the rank-64 "mid" update
+// of lu_trail_kernel restricted to [P + 64, P + 128)), and the rest of the matrix gets ONE rank-128
+// update: half the A22 traffic, 32 flop/B.  U12 = L11^-1 A12 for the 128 block rows is an MFMA
+// product with the explicitly inverted unit-lower L11 (lu_linv_kernel), fused into the trailing
+// update's prologue (every strip's workgroup owns its 128 columns of A12 and A22, so no other
+// workgroup reads what it overwrites).
+constexpr int kOB = 2 * kBlk;     // outer block width = rank of the fused trailing update
+constexpr int kT2C = 128;         // trailing update: columns per workgroup strip
+constexpr int kT2S = 64;          //   rows per pipeline step
+constexpr int kT2K = kOB + 4;     //   LDS stride (k) of the U12^T, -L21 and L11^-1 tiles
+constexpr int kT2CS = kT2C + 8;   //   LDS stride of the A22 staging tile
+constexpr int kT2Threads = 512;
+constexpr size_t kT2Lds = ((size_t)kT2C * kT2K + (size_t)kT2S * kT2K + (size_t)kT2S * kT2CS) * sizeof(float);
+static_assert(kT2S * kT2K + kT2S * kT2CS >= kOB * kT2K, "L11^-1 staging must fit in the -L21 + A22 tiles");
+static_assert(kT2Lds <= 160 * 1024, "gfx950 LDS");
+constexpr int kLinvFloats = kOB * kOB;
+
+// Linv[b] = (unit lower part of A[P:P+128, P:P+128])^-1, row-major 128 x 128.  Column j of the inverse
+// (thread j) by forward substitution x_i = -sum_{j<=k<i} L_ik x_k, x_j = 1, with L and X in LDS.
+__global__ __launch_bounds__(kOB) void lu_linv_kernel(int N, int P, const float* A, float* Linv) {
+  __shared__ float L[kOB][kOB + 1];
+  __shared__ float X[kOB][kOB + 1];
+  const int tid = threadIdx.x;
+  const size_t b = blockIdx.x;
+  const float* Ab = A + b * (size_t)N * N;
+  for (int idx = tid; idx < kOB * kOB; idx += blockDim.x) {
+    const int r = idx / kOB, c = idx % kOB;
+    L[r][c] = c < r ? Ab[(size_t)(P + r) * N + P + c] : 0.f;
+  }
+  __syncthreads();
+  const int j = tid;
+  for (int i = 0; i < kOB; ++i) {
+    float v;
+    if (i < j) {
+      v = 0.f;
+    } else if (i == j) {
+      v = 1.f;
+    } else {
+      v = 0.f;
+      for (int k = j; k < i; ++k) v = fmaf(L[i][k], X[k][j], v);
+      v = -v;
+    }
+    X[i][j] = v;
+  }
+  __syncthreads();
+  float* out = Linv + b * (size_t)kLinvFloats;
+  for (int idx = tid; idx < kOB * kOB; idx += blockDim.x) out[idx] = X[idx / kOB][idx % kOB];
+}
+
+// Fused U12 = L11^-1 A12 and A22 -= L21 U12 (rank 128) for the columns right of [P, P + 128).  One
+// workgroup (8 waves, one per CU) per (instance, 128-column strip), all trailing rows:
+//   prologue: A12 (128 x 128, transposed) and L11^-1 into LDS, U12 on MFMA (each wave two 32 x 32
+//             tiles), written to the block rows of A (final U) and, transposed, into Ut;
+//   main loop: 64-row steps, A22 through the LDS staging tile (row-contiguous 16-B global accesses),
+//             -L21 through LDS, next step's A22 / L21 loads in flight during the MFMAs; wave
+//             (wr, wc) owns 32 x 32 of a step (v_mfma_f32_32x32x2f32, 64 per step: lane half h covers
+//             k in [64h, 64h + 64)).
+// Strips of one instance are consecutive logical ids on one XCD (its L2 serves the L21 re-reads).
+template <bool VEC>
+__global__ __launch_bounds__(kT2Threads, 1) void lu_trail128_kernel(int N, int P, int ntc, float* A,
+                                                                    const float* Linv) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  float* Ut = sm;                       // [kT2C cols][kT2K]: U12^T (A12^T in the prologue)
+  float* Ls = Ut + kT2C * kT2K;         // [kT2S rows][kT2K]: -L21 of the step
+  float* Cb = Ls + kT2S * kT2K;         // [kT2S rows][kT2CS]: A22 rows in, results out
+  float* Li = Ls;                       // prologue: L11^-1 [128 rows][kT2K] over Ls + Cb
+  const int nwg = gridDim.x, bid = blockIdx.x;
+  const int xcd = bid & 7, local = bid >> 3, q8 = nwg >> 3, r8 = nwg & 7;
+  const int logical = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + local;
+  const size_t b = (size_t)(logical / ntc);
+  const int tc = logical % ntc;
+  float* Ab = A + b * (size_t)N * N;
+  const int c0 = P + kOB, cb = c0 + tc * kT2C;
+  const int nsteps = (N - c0 + kT2S - 1) / kT2S;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, il = lane & 31, h = lane >> 5;
+  constexpr int NT = kT2Threads;
+
+  typedef typename std::conditional<VEC, float4, float>::type VT;
+  constexpr int W = VEC ? 4 : 1;
+  constexpr int kCQ = kT2S * kT2C / W / NT;   // A22 accesses per thread per step
+  constexpr int kLQ = kT2S * kOB / W / NT;    // -L21 accesses per thread per step
+  constexpr int kPQ = kOB * kT2C / W / NT;    // A12 / L11^-1 accesses per thread (prologue)
+  constexpr int CPR = kT2C / W, LPR = kOB / W;
+  auto ld = [&](int row, int col, bool ok) -> VT {
+    const float* p = Ab + (size_t)row * N + col;
+    if constexpr (VEC) {
+      const float4 x = *reinterpret_cast<const float4*>(p);
+      return ok ? x : make_float4(0.f, 0.f, 0.f, 0.f);
+    } else {
+      const float x = *p;
+      return ok ? x : 0.f;
+    }
+  };
+  auto st_lds = [&](float* d, const VT& v, float sgn) {
+    if constexpr (VEC) *reinterpret_cast<float4*>(d) = make_float4(sgn * v.x, sgn * v.y, sgn * v.z, sgn * v.w);
+    else *d = sgn * v;
+  };
+
+  // ---- prologue: U12 = L11^-1 A12 on this strip
+#pragma unroll
+  for (int q = 0; q < kPQ; ++q) {  // A12 -> Ut (transposed)
+    const int e = tid + NT * q, k = e / CPR, cl = (e % CPR) * W, col = cb + cl;
+    const VT u = ld(P + k, min(col, N - W), col < N);
+    if constexpr (VEC) {
+      Ut[(cl + 0) * kT2K + k] = u.x; Ut[(cl + 1) * kT2K + k] = u.y;
+      Ut[(cl + 2) * kT2K + k] = u.z; Ut[(cl + 3) * kT2K + k] = u.w;
+    } else {
+      Ut[cl * kT2K + k] = u;
+    }
+  }
+  const float* Lb = Linv + b * (size_t)kLinvFloats;
+#pragma unroll
+  for (int q = 0; q < kOB * kOB / 4 / NT; ++q) {  // L11^-1 -> Li (rows, 16-B pieces)
+    const int e = tid + NT * q, i = e / (kOB / 4), kk = (e % (kOB / 4)) * 4;
+    *reinterpret_cast<float4*>(Li + i * kT2K + kk) = *reinterpret_cast<const float4*>(Lb + (size_t)i * kOB + kk);
+  }
+  __syncthreads();
+  {
+    const int ti = wave >> 1, tj0 = 2 * (wave & 1);
+    floatx16 u0, u1;
+#pragma unroll
+    for (int v = 0; v < 16; ++v) { u0[v] = 0.f; u1[v] = 0.f; }
+#pragma unroll 4
+    for (int sg = 0; sg < kOB / 8; ++sg) {
+      const float4 fa = *reinterpret_cast<const float4*>(Li + (ti * 32 + il) * kT2K + (kOB / 2) * h + 4 * sg);
+      const float4 f0 = *reinterpret_cast<const float4*>(Ut + (tj0 * 32 + il) * kT2K + (kOB / 2) * h + 4 * sg);
+      const float4 f1 = *reinterpret_cast<const float4*>(Ut + (tj0 * 32 + 32 + il) * kT2K + (kOB / 2) * h + 4 * sg);
+#pragma unroll
+      for (int s4 = 0; s4 < 4; ++s4) {
+        u0 = __builtin_amdgcn_mfma_f32_32x32x2f32(get4(fa, s4), get4(f0, s4), u0, 0, 0, 0);
+        u1 = __builtin_amdgcn_mfma_f32_32x32x2f32(get4(fa, s4), get4(f1, s4), u1, 0, 0, 0);
+      }
+    }
+    __syncthreads();  // A12^T and L11^-1 consumed
+    // accumulator v <-> row ti*32 + 8(v/4) + 4h + v%4 of U12, column tj*32 + il of the strip
+#pragma unroll
+    for (int v = 0; v < 16; ++v) {
+      const int i = ti * 32 + 8 * (v >> 2) + 4 * h + (v & 3);
+      const int j0 = tj0 * 32 + il, j1 = j0 + 32;
+      Ut[j0 * kT2K + i] = u0[v];
+      Ut[j1 * kT2K + i] = u1[v];
+      if (cb + j0 < N) Ab[(size_t)(P + i) * N + cb + j0] = u0[v];
+      if (cb + j1 < N) Ab[(size_t)(P + i) * N + cb + j1] = u1[v];
+    }
+  }
+
+  // ---- main loop: A22 -= L21 U12
+  const int wr = (wave >> 2) * 32, wc = (wave & 3) * 32;
+  auto loadC = [&](int step, VT (&c)[kCQ]) {
+#pragma unroll
+    for (int q = 0; q < kCQ; ++q) {
+      const int e = tid + NT * q, row = c0 + step * kT2S + e / CPR, col = cb + (e % CPR) * W;
+      c[q] = ld(min(row, N - 1), min(col, N - W), row < N && col < N);
+    }
+  };
+  auto loadL = [&](int step, VT (&l)[kLQ]) {
+#pragma unroll
+    for (int q = 0; q < kLQ; ++q) {
+      const int e = tid + NT * q, row = c0 + step * kT2S + e / LPR;
+      l[q] = ld(min(row, N - 1), P + (e % LPR) * W, row < N);
+    }
+  };
+  auto writeCL = [&](const VT (&c)[kCQ], const VT (&l)[kLQ]) {
+#pragma unroll
+    for (int q = 0; q < kCQ; ++q) {
+      const int e = tid + NT * q;
+      st_lds(Cb + (e / CPR) * kT2CS + (e % CPR) * W, c[q], 1.f);
+    }
+#pragma unroll
+    for (int q = 0; q < kLQ; ++q) {
+      const int e = tid + NT * q;
+      st_lds(Ls + (e / LPR) * kT2K + (e % LPR) * W, l[q], -1.f);
+    }
+  };
+  auto storeOut = [&](int step) {
+#pragma unroll
+    for (int q = 0; q < kCQ; ++q) {
+      const int e = tid + NT * q, row = c0 + step * kT2S + e / CPR, col = cb + (e % CPR) * W;
+      if (row < N && col < N) {
+        const float* src = Cb + (e / CPR) * kT2CS + (e % CPR) * W;
+        if constexpr (VEC) *reinterpret_cast<float4*>(Ab + (size_t)row * N + col) = *reinterpret_cast<const float4*>(src);
+        else Ab[(size_t)row * N + col] = *src;
+      }
+    }
+  };
+
+  VT cr[kCQ], lr[kLQ];
+  loadC(0, cr);
+  loadL(0, lr);
+  writeCL(cr, lr);  // Ls / Cb: the prologue's last reads of Li finished before the barrier above
+  __syncthreads();
+  for (int step = 0; step < nsteps; ++step) {
+    const bool more = step + 1 < nsteps;
+    floatx16 acc;
+#pragma unroll
+    for (int v = 0; v < 16; ++v) acc[v] = Cb[(wr + 8 * (v >> 2) + 4 * h + (v & 3)) * kT2CS + wc + il];
+    if (more) {
+      loadC(step + 1, cr);
+      loadL(step + 1, lr);
+    }
+#pragma unroll 4
+    for (int sg = 0; sg < kOB / 8; ++sg) {
+      const float4 fa = *reinterpret_cast<const float4*>(Ls + (wr + il) * kT2K + (kOB / 2) * h + 4 * sg);
+      const float4 fb = *reinterpret_cast<const float4*>(Ut + (wc + il) * kT2K + (kOB / 2) * h + 4 * sg);
+#pragma unroll
+      for (int s4 = 0; s4 < 4; ++s4) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(get4(fa, s4), get4(fb, s4), acc, 0, 0, 0);
+    }
+    __syncthreads();  // Cb (this step's A22) and Ls consumed by every wave
+#pragma unroll
+    for (int v = 0; v < 16; ++v) Cb[(wr + 8 * (v >> 2) + 4 * h + (v & 3)) * kT2CS + wc + il] = acc[v];
+    __syncthreads();
+    storeOut(step);
+    __syncthreads();  // Cb drained
+    if (more) writeCL(cr, lr);
+    __syncthreads();
   }
 }
 
@@ -644,66 +868,119 @@ __global__ void kkt_rhs_kernel(int64_t B, int n, int m, int num_ineq, const floa
 
 using namespace iadmm;
 
-static int lu_factor_blocks(int64_t B, int64_t N, float* A, int* piv, int* info, int* perm, hipStream_t s) {
-  const bool vec = (N % 4 == 0) && aligned16(A);
-  IADMM_ALLOW_LDS(lu_trail_kernel<true>, kTrailLds);
-  IADMM_ALLOW_LDS(lu_trail_kernel<false>, kTrailLds);
-  for (int K0 = 0; K0 < N; K0 += kBlk) {
-    const int cend = (int)std::min<int64_t>(N, K0 + kBlk);
-    if (N <= kPanelMaxM * kLuThreads) {
-      for (int k0 = K0; k0 < cend; k0 += kNB) {
-        const int R = (int)N - k0;
-        const dim3 g((unsigned)B), t(kLuThreads);
-        if (R <= kLuThreads) hipLaunchKernelGGL((lu_panel_kernel<1, kNB, kLuThreads>), g, t, 0, s, (int)N, K0, k0, cend, A, piv, info);
-        else if (R <= 2 * kLuThreads) hipLaunchKernelGGL((lu_panel_kernel<2, kNB, kLuThreads>), g, t, 0, s, (int)N, K0, k0, cend, A, piv, info);
-        else if (R <= 4 * kLuThreads) hipLaunchKernelGGL((lu_panel_kernel<4, kNB, kLuThreads>), g, t, 0, s, (int)N, K0, k0, cend, A, piv, info);
-        else hipLaunchKernelGGL((lu_panel_kernel<kPanelMaxM, kNB, kLuThreads>), g, t, 0, s, (int)N, K0, k0, cend, A, piv, info);
+// Panels (+ in-block updates) of the 64-column half [K0, cend).
+static int lu_factor_half(int64_t B, int64_t N, int K0, int cend, float* A, int* piv, int* info, hipStream_t s) {
+  if (N <= kPanelMaxM * kLuThreads) {
+    for (int k0 = K0; k0 < cend; k0 += kNB) {
+      const int R = (int)N - k0;
+      const dim3 g((unsigned)B), t(kLuThreads);
+      if (R <= kLuThreads) hipLaunchKernelGGL((lu_panel_kernel<1, kNB, kLuThreads>), g, t, 0, s, (int)N, K0, k0, cend, A, piv, info);
+      else if (R <= 2 * kLuThreads) hipLaunchKernelGGL((lu_panel_kernel<2, kNB, kLuThreads>), g, t, 0, s, (int)N, K0, k0, cend, A, piv, info);
+      else if (R <= 4 * kLuThreads) hipLaunchKernelGGL((lu_panel_kernel<4, kNB, kLuThreads>), g, t, 0, s, (int)N, K0, k0, cend, A, piv, info);
+      else hipLaunchKernelGGL((lu_panel_kernel<kPanelMaxM, kNB, kLuThreads>), g, t, 0, s, (int)N, K0, k0, cend, A, piv, info);
+      IADMM_CHECK_LAUNCH();
+      const int c0 = k0 + kNB;
+      if (c0 < cend) {
+        const dim3 grid((unsigned)B, (unsigned)((N - c0 + kUpdRows - 1) / kUpdRows));
+        hipLaunchKernelGGL(lu_update_block_kernel<kNB>, grid, dim3(256), 0, s, (int)N, k0, cend, A);
         IADMM_CHECK_LAUNCH();
-        const int c0 = k0 + kNB;
-        if (c0 < cend) {
-          const dim3 grid((unsigned)B, (unsigned)((N - c0 + kUpdRows - 1) / kUpdRows));
-          hipLaunchKernelGGL(lu_update_block_kernel<kNB>, grid, dim3(256), 0, s, (int)N, k0, cend, A);
-          IADMM_CHECK_LAUNCH();
-        }
-      }
-    } else {  // N > 2048: 8-wide panels on 1024-thread workgroups (N <= kBigMaxM * kBigThreads)
-      for (int k0 = K0; k0 < cend; k0 += kBigNB) {
-        const int R = (int)N - k0;
-        const dim3 g((unsigned)B), t(kBigThreads);
-        if (R <= 2 * kBigThreads) hipLaunchKernelGGL((lu_panel_kernel<2, kBigNB, kBigThreads>), g, t, 0, s, (int)N, K0, k0, cend, A, piv, info);
-        else if (R <= 4 * kBigThreads) hipLaunchKernelGGL((lu_panel_kernel<4, kBigNB, kBigThreads>), g, t, 0, s, (int)N, K0, k0, cend, A, piv, info);
-        else if (R <= 8 * kBigThreads) hipLaunchKernelGGL((lu_panel_kernel<8, kBigNB, kBigThreads>), g, t, 0, s, (int)N, K0, k0, cend, A, piv, info);
-        else hipLaunchKernelGGL((lu_panel_kernel<kBigMaxM, kBigNB, kBigThreads>), g, t, 0, s, (int)N, K0, k0, cend, A, piv, info);
-        IADMM_CHECK_LAUNCH();
-        const int c0 = k0 + kBigNB;
-        if (c0 < cend) {
-          const dim3 grid((unsigned)B, (unsigned)((N - c0 + kUpdRows - 1) / kUpdRows));
-          hipLaunchKernelGGL(lu_update_block_kernel<kBigNB>, grid, dim3(256), 0, s, (int)N, k0, cend, A);
-          IADMM_CHECK_LAUNCH();
-        }
       }
     }
-    const int outside = K0 + ((int)N - cend);
-    if (outside > 0) {
-      hipLaunchKernelGGL(lu_block_perm_kernel, dim3((unsigned)B), dim3(64), 0, s, (int)N, K0, cend, piv, perm);
+  } else {  // N > 2048: 8-wide panels on 1024-thread workgroups (N <= kBigMaxM * kBigThreads)
+    for (int k0 = K0; k0 < cend; k0 += kBigNB) {
+      const int R = (int)N - k0;
+      const dim3 g((unsigned)B), t(kBigThreads);
+      if (R <= 2 * kBigThreads) hipLaunchKernelGGL((lu_panel_kernel<2, kBigNB, kBigThreads>), g, t, 0, s, (int)N, K0, k0, cend, A, piv, info);
+      else if (R <= 4 * kBigThreads) hipLaunchKernelGGL((lu_panel_kernel<4, kBigNB, kBigThreads>), g, t, 0, s, (int)N, K0, k0, cend, A, piv, info);
+      else if (R <= 8 * kBigThreads) hipLaunchKernelGGL((lu_panel_kernel<8, kBigNB, kBigThreads>), g, t, 0, s, (int)N, K0, k0, cend, A, piv, info);
+      else hipLaunchKernelGGL((lu_panel_kernel<kBigMaxM, kBigNB, kBigThreads>), g, t, 0, s, (int)N, K0, k0, cend, A, piv, info);
       IADMM_CHECK_LAUNCH();
-      hipLaunchKernelGGL(lu_swap_trsm_block_kernel, dim3((unsigned)B, (unsigned)((outside + 255) / 256)), dim3(256), 0,
-                         s, (int)N, K0, cend, A, perm);
-      IADMM_CHECK_LAUNCH();
-    }
-    if (cend < N) {
-      const int rest = (int)N - cend;
-      const int ntc = (rest + kTC - 1) / kTC, nrc = (rest + kTRW - 1) / kTRW;
-      const dim3 grid((unsigned)(B * ntc * nrc));
-      if (vec) hipLaunchKernelGGL(lu_trail_kernel<true>, grid, dim3(kTrailThreads), kTrailLds, s, (int)N, K0, ntc, nrc, A);
-      else hipLaunchKernelGGL(lu_trail_kernel<false>, grid, dim3(kTrailThreads), kTrailLds, s, (int)N, K0, ntc, nrc, A);
-      IADMM_CHECK_LAUNCH();
+      const int c0 = k0 + kBigNB;
+      if (c0 < cend) {
+        const dim3 grid((unsigned)B, (unsigned)((N - c0 + kUpdRows - 1) / kUpdRows));
+        hipLaunchKernelGGL(lu_update_block_kernel<kBigNB>, grid, dim3(256), 0, s, (int)N, k0, cend, A);
+        IADMM_CHECK_LAUNCH();
+      }
     }
   }
   return 0;
 }
 
-static int64_t lu_ws_bytes(int64_t B) { return B * (int64_t)kPermInts * (int64_t)sizeof(int); }
+// The half's row interchanges on every column outside [K0, cend), with U12 = L11^-1 A12 for the
+// columns [cend, trsm_end).
+static int lu_swap_half(int64_t B, int64_t N, int K0, int cend, int trsm_end, float* A, const int* piv, int* perm,
+                        hipStream_t s) {
+  const int outside = K0 + ((int)N - cend);
+  if (outside <= 0) return 0;
+  hipLaunchKernelGGL(lu_block_perm_kernel, dim3((unsigned)B), dim3(64), 0, s, (int)N, K0, cend, piv, perm);
+  IADMM_CHECK_LAUNCH();
+  hipLaunchKernelGGL(lu_swap_trsm_block_kernel, dim3((unsigned)B, (unsigned)((outside + 255) / 256)), dim3(256), 0, s,
+                     (int)N, K0, cend, trsm_end, A, perm);
+  IADMM_CHECK_LAUNCH();
+  return 0;
+}
+
+// rank-64 update A[cend.., cend..cmax) -= L21 U12 of the half [K0, cend) (lu_trail_kernel)
+static int lu_rank64(int64_t B, int64_t N, int K0, int cend, int cmax, float* A, bool vec, hipStream_t s) {
+  const int rest = (int)N - cend, wid = cmax - cend;
+  if (rest <= 0 || wid <= 0) return 0;
+  const int ntc = (wid + kTC - 1) / kTC, nrc = (rest + kTRW - 1) / kTRW;
+  const dim3 grid((unsigned)(B * ntc * nrc));
+  if (vec) hipLaunchKernelGGL(lu_trail_kernel<true>, grid, dim3(kTrailThreads), kTrailLds, s, (int)N, K0, ntc, nrc, cmax, A);
+  else hipLaunchKernelGGL(lu_trail_kernel<false>, grid, dim3(kTrailThreads), kTrailLds, s, (int)N, K0, ntc, nrc, cmax, A);
+  IADMM_CHECK_LAUNCH();
+  return 0;
+}
+
+#ifndef IADMM_LU_RANK128
+#define IADMM_LU_RANK128 1   // 0: the r02 flow (rank-64 trailing update per 64 columns; tools A/B only)
+#endif
+
+static int lu_factor_blocks(int64_t B, int64_t N, float* A, int* piv, int* info, int* perm, float* linv,
+                            hipStream_t s) {
+  const bool vec = (N % 4 == 0) && aligned16(A);
+  IADMM_ALLOW_LDS(lu_trail_kernel<true>, kTrailLds);
+  IADMM_ALLOW_LDS(lu_trail_kernel<false>, kTrailLds);
+  IADMM_ALLOW_LDS(lu_trail128_kernel<true>, kT2Lds);
+  IADMM_ALLOW_LDS(lu_trail128_kernel<false>, kT2Lds);
+  int rc = 0;
+  if (!IADMM_LU_RANK128) {
+    for (int K0 = 0; K0 < N && !rc; K0 += kBlk) {
+      const int cend = (int)std::min<int64_t>(N, K0 + kBlk);
+      rc = lu_factor_half(B, N, K0, cend, A, piv, info, s);
+      if (!rc) rc = lu_swap_half(B, N, K0, cend, (int)N, A, piv, perm, s);
+      if (!rc) rc = lu_rank64(B, N, K0, cend, (int)N, A, vec, s);
+    }
+    return rc;
+  }
+  for (int P = 0; P < N && !rc; P += kOB) {
+    const int c1 = (int)std::min<int64_t>(N, P + kBlk), c2 = (int)std::min<int64_t>(N, P + kOB);
+    // first half: factor, interchanges everywhere else, U12 for the second half's columns only, and
+    // the second half's rank-64 update
+    rc = lu_factor_half(B, N, P, c1, A, piv, info, s);
+    if (!rc) rc = lu_swap_half(B, N, P, c1, c2, A, piv, perm, s);
+    if (!rc) rc = lu_rank64(B, N, P, c1, c2, A, vec, s);
+    if (rc || c1 >= N) break;
+    // second half: factor, interchanges everywhere else (no substitution)
+    rc = lu_factor_half(B, N, c1, c2, A, piv, info, s);
+    if (!rc) rc = lu_swap_half(B, N, c1, c2, c2, A, piv, perm, s);
+    if (rc || c2 >= N) break;
+    // U12 = L11^-1 A12 and the rank-128 update of everything right of the block
+    hipLaunchKernelGGL(lu_linv_kernel, dim3((unsigned)B), dim3(kOB), 0, s, (int)N, P, A, linv);
+    IADMM_CHECK_LAUNCH();
+    const int ntc = ((int)N - c2 + kT2C - 1) / kT2C;
+    const dim3 grid((unsigned)(B * ntc));
+    if (vec) hipLaunchKernelGGL(lu_trail128_kernel<true>, grid, dim3(kT2Threads), kT2Lds, s, (int)N, P, ntc, A, linv);
+    else hipLaunchKernelGGL(lu_trail128_kernel<false>, grid, dim3(kT2Threads), kT2Lds, s, (int)N, P, ntc, A, linv);
+    IADMM_CHECK_LAUNCH();
+  }
+  return rc;
+}
+
+// workspace: per-instance block permutations (kPermInts ints) + the 128 x 128 L11^-1 of the current
+// outer block (16-B aligned after the permutations)
+static int64_t lu_perm_bytes(int64_t B) { return ((B * (int64_t)kPermInts * (int64_t)sizeof(int)) + 15) / 16 * 16; }
+static int64_t lu_ws_bytes(int64_t B) { return lu_perm_bytes(B) + B * (int64_t)kLinvFloats * (int64_t)sizeof(float); }
 
 extern "C" int64_t iadmm_lu_factor_ws_bytes(int64_t B, int64_t N) {
   if (B <= 0 || N <= 0) return 0;
@@ -721,7 +998,9 @@ extern "C" int iadmm_lu_factor(int64_t B, int64_t N, float* A, int* piv, int* in
   hipStream_t s = (hipStream_t)stream;
   const hipError_t e = hipMemsetAsync(info, 0, B * sizeof(int), s);
   if (e != hipSuccess) return (int)e;
-  return lu_factor_blocks(B, N, A, piv, info, static_cast<int*>(ws), s);  // ws: per-instance block permutations
+  int* perm = static_cast<int*>(ws);
+  float* linv = reinterpret_cast<float*>(static_cast<char*>(ws) + lu_perm_bytes(B));
+  return lu_factor_blocks(B, N, A, piv, info, perm, linv, s);
 }
 
 extern "C" int iadmm_lu_solve(int64_t B, int64_t N, const float* LU, const int* piv, float* x,

@@ -397,8 +397,10 @@ def stage2(Q, p, A0, zl, zu, rho_rows, x, y, z, sigma, iters, alpha=STAGE2_ALPHA
         Qc, pc, Ac, zlc, zuc, rc = (t[sl] for t in (Q, p, A0, zl, zu, rho_rows))
         xc, yc, zc = x[sl], y[sl], z[sl]
         LU = piv = None  # the previous chunk's factors are released before the next K is built
-        tok = timer.start("stage2_factor")
+        tok = timer.start("stage2_assemble")
         K = ops.kkt_assemble(Qc, Ac, sigma, None, 0, rho_rows=rc)
+        timer.stop(tok)
+        tok = timer.start("stage2_factor")
         LU, piv, info = ops.lu_factor(K)
         timer.stop(tok)
         bad = int(info.max())  # one host read per factorisation

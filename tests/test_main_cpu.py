@@ -10,7 +10,7 @@ from conftest import PKG
 
 # the reference times Ruiz scaling, the model() calls, the final unscale and Stage II; it does
 # not time the zero-fills of the state (allocated before start_time, main.py:836-841) or metrics
-TIMED = {"scaling", "iterations", "unscale", "stage2_factor", "stage2_iterations"}
+TIMED = {"scaling", "iterations", "unscale", "stage2_assemble", "stage2_factor", "stage2_iterations"}
 
 
 def _span_names():

@@ -162,3 +162,21 @@ def test_stage2_golden(golden):
     K = orc.kkt_matrix(torch.from_numpy(g["in_Q"]), torch.from_numpy(g["in_A0"]), float(g["sigma"]),
                        torch.from_numpy(g["fin_rhovec"]))
     assert rel_l2(A_t.dense(), K) < 1e-7
+
+
+# n, m multiples of 4 -> the 16-B row-band kernel (n % 32 != 0: a band straddling the Q / A0 rows;
+# m > 256: several LDS chunks of the A0^T block); otherwise the 64 x 64 tile kernel
+@pytest.mark.parametrize("n,m", [(1000, 1000), (100, 300), (36, 20), (64, 0), (37, 15), (24, 12), (40, 6)])
+def test_kkt_assemble_bitwise(n, m):
+    """iadmm_kkt_assemble builds exactly the reference's K (models/lu.py:27-28 / models/lstm.py:67-68:
+    copies, one sigma add per diagonal, -(1/rho) on the lower-right diagonal, -0 elsewhere)."""
+    from iadmm import ops
+    from oracle import iadmm_oracle as orc
+    B = 2
+    g = torch.Generator().manual_seed(n + m)
+    Q, A0 = torch.randn(B, n, n, generator=g), torch.randn(B, m, n, generator=g)
+    rho = torch.rand(B, m, generator=g) + 0.05
+    K = ops.kkt_assemble(Q.cuda(), A0.cuda(), 6e-6, None, 0, rho_rows=rho.cuda())
+    ref = orc.kkt_matrix(Q, A0, 6e-6, rho.unsqueeze(-1))
+    assert torch.equal(K.cpu(), ref)
+    assert torch.equal(torch.signbit(K.cpu()), torch.signbit(ref))
