@@ -103,6 +103,24 @@ def pmc_traffic(kernel_prefix, n, m, h, B, lanes=1):
     return tot
 
 
+def rocprof_avg_ms(kernels, tag_glob="r*_bench_kernel_stats.csv"):
+    """Sum of the rocprofv3 --stats average durations (ms) of ``kernels`` (name substrings) in the
+    newest committed bench kernel-stats profile, with the file name; (None, None) without one."""
+    import csv
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", tag_glob)))  # r01 < r02 < r02final < r03
+    for f in reversed(files):
+        rows = list(csv.DictReader(open(f)))
+        got = {}
+        for k in kernels:
+            hit = [r for r in rows if k in r["Name"]]
+            if hit:
+                got[k] = float(hit[0]["AverageNs"]) / 1e6
+        if len(got) == len(kernels):
+            return sum(got.values()), os.path.relpath(f, ROOT)
+    return None, None
+
+
 def pmc_traffic_stage2(n, m, B):
     """HBM bytes of one factorization (every lu_* kernel but the solve) from the committed Stage-II
     PMC summaries of tools/profile_lu.py (one factorization; tools/pmc_summary.py: per-kernel mean
@@ -192,6 +210,8 @@ def cpu_baseline(args, d, params, gpu_out, weights_tag, extra=()):
     cpu = {k: d[k][:Bc].cpu() for k in ("Q", "p", "A0", "zl", "zu")}
     out, dt = run_oracle(args, cpu, params)
     rec = dict(value=Bc / dt, unit="QP instances/s", cores=threads, kind="port", cpu_model=cpu_model(),
+               cores_note=f"torch.set_num_threads({threads}) from OMP_NUM_THREADS: the GPU box sets it to the CPU "
+                          f"share of one GPU's lease (16); os.cpu_count() = {os.cpu_count()} counts the whole host",
                sample=f"{Bc} instances x full solve (Ruiz + K={args.outer_T} + unscale), the same synthetic "
                       f"instances 0..{Bc - 1} and weights ({weights_tag}) as the GPU run, {dt:.1f} s; "
                       f"8 of config 1's 64 instances (CPU cost is linear in the batch)",
@@ -487,6 +507,15 @@ def main():
         out = out_keep
         torch.cuda.empty_cache()
 
+    # the same roofline from the committed rocprof profile of this workload (another run: rocprof
+    # serialises and times each of the four kernels; the hipEvent span above brackets them back to back)
+    kkt_rocprof = None
+    if (n, mi, me, h, B) == (1000, 500, 500, 800, 1024):
+        ms_rp, src = rocprof_avg_ms(KKT_KERNELS)
+        if ms_rp:
+            gbs = kkt_bytes / (ms_rp * 1e-3) / 1e9
+            kkt_rocprof = {"avg_launch_ms": ms_rp, "achieved": gbs, "frac": gbs / HBM_PEAK_GBS, "source": src}
+
     res = None
     if rank == 0:
         total = world * B * args.steps
@@ -522,6 +551,8 @@ def main():
                                 "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": kkt_gbs / HBM_PEAK_GBS,
                                 "traffic": pmc_traffic(KKT_KERNELS, n, mi + me, h, B, lanes),
                                 "kernels": "kkt_split_p1 + c1 + p2 + c2 (row-block split, csrc/kkt.hip)",
+                                "timing": "hipEvents around the four launches of each call, this run",
+                                "rocprof": kkt_rocprof,
                                 "avg_launch_ms": ms_kkt, "launches": n_kkt, "busy_ms_per_iteration": busy_kkt / iters,
                                 "algorithmic_per_iteration": kkt_bytes,
                                 "algorithmic_per_launch": kkt_bytes / lanes},

@@ -57,6 +57,7 @@ def build_parser():
     add("--random_init", action="store_true", help="random-init weights when no checkpoint exists")
     add("--data_dir", type=str, default="./datasets")
     add("--micro_batch", type=int, default=0, help="instances per forward/backward pass (memory)")
+    add("--max_minutes", type=float, default=0.0, help="train: stop after the epoch that exceeds this wall time")
     return p
 
 
@@ -328,6 +329,7 @@ def run_train(args):
     train_ids, val_ids, _ = split_ids(args)
     packed = solver.PackedWeights()
     history = []
+    t_start = time.time()
     for epoch in range(args.num_epoch):
         model.train()
         t0 = time.time()
@@ -352,6 +354,9 @@ def run_train(args):
             if bi == n_batches - 1:  # only the epoch's last batch is reported (main.py:362-379)
                 last = dict(d=d, x=fin["x"].reshape(count, -1) * (Dsc.reshape(count, -1) if Dsc is not None else 1.0))
             del d, ds, fin
+            if rank == 0 and (bi + 1) % 50 == 0:
+                print(f"[train] epoch {epoch} batch {bi + 1}/{n_batches} loss {loss:.4f} "
+                      f"{time.time() - t0:.0f} s", file=sys.stderr, flush=True)
         train_time = time.time() - t0
         # main.py:362-379: objective and violations of the last training batch's final iterate
         # (unscaled); each rank holds its shard, so the means are combined over ranks
@@ -370,6 +375,8 @@ def run_train(args):
         stop = False
         if rank == 0:
             stop = stopper.step(val_obj, model, args.early_stop_mode or "min", args.eq_tol, *vios)
+            if args.max_minutes and time.time() - t_start > 60.0 * args.max_minutes:
+                stop = True  # decided on rank 0 and broadcast below, like the early stop
             tobj = tr["obj"] if tr else float("nan")
             print("Epoch : {} | Train_Obj : {:.3f} | Val_Obj : {:.3f} | Train_Time : {:.3f} | Val_Time : {:.3f} |".format(
                 epoch, tobj, val_obj, train_time, val_time), flush=True)

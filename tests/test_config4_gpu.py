@@ -132,6 +132,7 @@ def test_config4_full_batch_matches_single_instances():
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     from iadmm import data, solver
+    torch.cuda.empty_cache()  # ~230 GB of the 288 below: start from an empty caching allocator
     params = data.init_lstm_params(H, LENGTH, device="cuda")
     keys = ("x", "y", "z", "xv", "primal", "dual", "obj")
     d = data.make_qp_batch(N_VAR, MI, ME, B_FULL, first_index=0, device="cuda")
