@@ -267,6 +267,217 @@ __global__ __launch_bounds__(NT, NT <= 256 ? 2 : 1) void lu_panel_kernel(int N, 
   }
 }
 
+// Fused factorization of one 64-column half [K0, cend) in ONE launch (r03; r02 launched every NB-wide
+// sub-panel and every in-block update separately: 7 launches per half at N <= 2048).  One workgroup
+// per instance; thread t owns the rows K0 + t + NT m of the half for the whole launch.  Per sub-panel
+// k0 = K0 + NB j: load it (rows >= k0) into registers and factor it exactly as lu_panel_kernel does
+// (same pivot rule and operation order), write it back, apply its interchanges to the half's other
+// columns, U = L11^-1 A on its rows right of it inside the half (kept in LDS too), then the rank-NB
+// update of the half's columns right of it, rows >= k0 + NB, one NT-row chunk at a time: the chunk's
+// multipliers are staged in LDS by their row owners and the chunk is updated cooperatively with
+// accesses contiguous along the columns (as lu_update_block_kernel).  Same arithmetic per element as
+// the unfused kernels: the factors are bitwise those of the r02 sequence.
+template <int M, int NB, int NT>
+__global__ __launch_bounds__(NT, NT <= 256 ? 2 : 1) void lu_half_kernel(int N, int K0, int cend, float* A, int* piv,
+                                                                        int* info) {
+  constexpr int NWV = NT / 64;
+  __shared__ float xrow[2][NB];
+  __shared__ float L11[NB][NB + 1];
+  __shared__ float rv[NWV];
+  __shared__ int ri[NWV + 1];
+  __shared__ int pvs[NB], prow[2 * NB], pcur[2 * NB], pcnt[1];
+  __shared__ float Us[NB][kBlk];        // U rows of the sub-panel, columns of the half (relative to K0)
+  __shared__ float Lc[NT][NB + 1];      // multipliers of one NT-row chunk
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const size_t b = blockIdx.x;
+  float* Ab = A + b * (size_t)N * N;
+  const int R0 = N - K0;
+  float a[M][NB];
+  for (int k0 = K0; k0 < cend; k0 += NB) {
+    const int nb = min(NB, cend - k0);
+    const int j0 = k0 - K0;                       // rows [K0, k0) of the half are final
+    const bool vec = nb == NB && (N % 4) == 0 && aligned16(Ab) && (NB % 4) == 0;
+#pragma unroll
+    for (int m = 0; m < M; ++m) {
+      const int rr = tid + NT * m;
+      const bool live = rr >= j0 && rr < R0;
+      const float* src = Ab + (size_t)(K0 + min(max(rr, j0), R0 - 1)) * N + k0;
+      if (vec) {
+#pragma unroll
+        for (int c4 = 0; c4 < NB; c4 += 4) {
+          const float4 v = *reinterpret_cast<const float4*>(src + c4);
+          a[m][c4] = v.x; a[m][c4 + 1] = v.y; a[m][c4 + 2] = v.z; a[m][c4 + 3] = v.w;
+        }
+      } else {
+#pragma unroll
+        for (int c = 0; c < NB; ++c) a[m][c] = c < nb ? src[c] : 0.f;
+      }
+      if (!live) {
+#pragma unroll
+        for (int c = 0; c < NB; ++c) a[m][c] = 0.f;
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < NB; ++j) {
+      if (j < nb) {
+        const int jr = j0 + j;                    // row k0 + j, relative to K0: owned by thread jr, m = 0
+        float best = -1.f;
+        int bi = R0;
+#pragma unroll
+        for (int m = 0; m < M; ++m) {
+          const int rr = tid + NT * m;
+          const float v = fabsf(col_of(a[m], j));
+          if (rr >= jr && rr < R0 && v > best) { best = v; bi = rr; }
+        }
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) {
+          const float ov = __shfl_xor(best, o, 64);
+          const int oi = __shfl_xor(bi, o, 64);
+          if (ov > best || (ov == best && oi < bi)) { best = ov; bi = oi; }
+        }
+        if (lane == 0) { rv[wave] = best; ri[wave] = bi; }
+        if (tid == jr) {
+#pragma unroll
+          for (int c = 0; c < NB; ++c) xrow[0][c] = a[0][c];
+        }
+        __syncthreads();
+        if (tid == 0) {
+          float bv = rv[0];
+          int bx = ri[0];
+          for (int w = 1; w < NWV; ++w)
+            if (rv[w] > bv || (rv[w] == bv && ri[w] < bx)) { bv = rv[w]; bx = ri[w]; }
+          if (bx >= R0) bx = jr;  // all entries NaN: keep the diagonal
+          else if (bv == 0.f && info[b] == 0) info[b] = k0 + j + 1;
+          ri[NWV] = bx;
+          piv[b * N + k0 + j] = K0 + bx + 1;
+          pvs[j] = K0 + bx;
+        }
+        __syncthreads();
+        const int p = ri[NWV];
+#pragma unroll
+        for (int m = 0; m < M; ++m)
+          if (tid + NT * m == p) {
+#pragma unroll
+            for (int c = 0; c < NB; ++c) {
+              xrow[1][c] = a[m][c];
+              a[m][c] = xrow[0][c];
+            }
+          }
+        __syncthreads();
+        if (tid == jr) {
+#pragma unroll
+          for (int c = 0; c < NB; ++c) a[0][c] = xrow[1][c];
+        }
+        const float pv = xrow[1][j];
+        if (pv != 0.f) {
+          const float rcp = 1.0f / pv;
+          float pr[NB];
+#pragma unroll
+          for (int c = 0; c < NB; ++c) pr[c] = xrow[1][c];
+#pragma unroll
+          for (int m = 0; m < M; ++m) {
+            const int rr = tid + NT * m;
+            if (rr > jr && rr < R0) {
+              const float l = col_of(a[m], j) * rcp;
+#pragma unroll
+              for (int c = 0; c < NB; ++c) {
+                if (c == j) a[m][c] = l;
+                else if (c > j) a[m][c] = a[m][c] - l * pr[c];
+              }
+            }
+          }
+        }
+        __syncthreads();  // xrow is rewritten by the next column
+      }
+    }
+    // the factored sub-panel back to HBM; L11 for the substitution
+#pragma unroll
+    for (int m = 0; m < M; ++m) {
+      const int rr = tid + NT * m;
+      if (rr >= j0 && rr < R0) {
+        float* dst = Ab + (size_t)(K0 + rr) * N + k0;
+        if (vec) {
+#pragma unroll
+          for (int c4 = 0; c4 < NB; c4 += 4)
+            *reinterpret_cast<float4*>(dst + c4) = make_float4(a[m][c4], a[m][c4 + 1], a[m][c4 + 2], a[m][c4 + 3]);
+        } else {
+#pragma unroll
+          for (int c = 0; c < NB; ++c)
+            if (c < nb) dst[c] = a[m][c];
+        }
+      }
+    }
+    if (tid >= j0 && tid < j0 + nb) {
+#pragma unroll
+      for (int c = 0; c < NB; ++c) L11[tid - j0][c] = a[0][c];
+    }
+    // interchanges on the half's columns outside the sub-panel (lu_panel_kernel's ?laswp step)
+    build_row_perm(pvs, k0, nb, prow, pcur, pcnt);  // (its barrier also publishes L11 and the stores above)
+    {
+      const int cnt = *pcnt;
+      const int col = K0 + tid;
+      if (tid < kBlk && col < cend && (col < k0 || col >= k0 + nb)) {
+        float v[2 * NB];
+#pragma unroll
+        for (int i = 0; i < 2 * NB; ++i) v[i] = i < cnt ? Ab[(size_t)pcur[i] * N + col] : 0.f;
+#pragma unroll
+        for (int i = 0; i < 2 * NB; ++i)
+          if (i < cnt) Ab[(size_t)prow[i] * N + col] = v[i];
+      }
+    }
+    const int cr0 = k0 + nb;                      // first column right of the sub-panel
+    if (cr0 >= cend) break;                       // last sub-panel of the half: no update inside it
+    __syncthreads();
+    // U = L11^-1 A on the sub-panel rows, columns [cr0, cend) (one thread per column)
+    {
+      const int c = cr0 + tid;
+      if (tid < cend - cr0) {
+        float x[NB];
+#pragma unroll
+        for (int i = 0; i < NB; ++i) x[i] = i < nb ? Ab[(size_t)(k0 + i) * N + c] : 0.f;
+#pragma unroll
+        for (int i = 1; i < NB; ++i) {
+          float s = x[i];
+#pragma unroll
+          for (int l = 0; l < i; ++l) s = s - L11[i][l] * x[l];
+          x[i] = s;
+        }
+#pragma unroll
+        for (int i = 0; i < NB; ++i)
+          if (i < nb) {
+            Ab[(size_t)(k0 + i) * N + c] = x[i];
+            Us[i][c - K0] = x[i];
+          }
+      }
+    }
+    // rank-nb update of [cr0, cend) for the rows below the sub-panel, chunk by chunk
+    const int w = cend - cr0;
+#pragma unroll
+    for (int m = 0; m < M; ++m) {
+      const int rr = tid + NT * m;
+      __syncthreads();  // Us written / the previous chunk's Lc consumed
+#pragma unroll
+      for (int l = 0; l < NB; ++l) Lc[tid][l] = a[m][l];
+      __syncthreads();
+      const int rbeg = max(NT * m, j0 + nb), rend = min(NT * (m + 1), R0);
+      if (rbeg >= rend) continue;
+      const int rows = rend - rbeg, tot = rows * w;
+      (void)rr;
+      for (int idx = tid; idx < tot; idx += NT) {
+        const int r = idx / w, c = idx - r * w;
+        const int rl = rbeg + r;                  // row relative to K0
+        float* ap = Ab + (size_t)(K0 + rl) * N + cr0 + c;
+        float v = *ap;
+#pragma unroll
+        for (int l = 0; l < NB; ++l)
+          if (l < nb) v = v - Lc[rl - NT * m][l] * Us[l][cr0 - K0 + c];
+        *ap = v;
+      }
+    }
+    __syncthreads();  // the updated columns are re-read as the next sub-panel
+  }
+}
+
 // A[c0.., c0..cend) -= L21 U12 inside the current 64-column block, c0 = k0 + 16: rows
 // [c0 + blockIdx.y*64, +64) of instance blockIdx.x, w = cend - c0 <= 64 - NB columns.
 template <int NB>
@@ -868,8 +1079,31 @@ __global__ void kkt_rhs_kernel(int64_t B, int n, int m, int num_ineq, const floa
 
 using namespace iadmm;
 
+#ifndef IADMM_LU_FUSED_HALF
+#define IADMM_LU_FUSED_HALF 1   // 0: one launch per sub-panel and per in-block update (r02; tools A/B only)
+#endif
+
 // Panels (+ in-block updates) of the 64-column half [K0, cend).
 static int lu_factor_half(int64_t B, int64_t N, int K0, int cend, float* A, int* piv, int* info, hipStream_t s) {
+  if (IADMM_LU_FUSED_HALF) {
+    const int R = (int)N - K0;
+    const dim3 g((unsigned)B);
+    if (N <= kPanelMaxM * kLuThreads) {
+      const dim3 t(kLuThreads);
+      if (R <= kLuThreads) hipLaunchKernelGGL((lu_half_kernel<1, kNB, kLuThreads>), g, t, 0, s, (int)N, K0, cend, A, piv, info);
+      else if (R <= 2 * kLuThreads) hipLaunchKernelGGL((lu_half_kernel<2, kNB, kLuThreads>), g, t, 0, s, (int)N, K0, cend, A, piv, info);
+      else if (R <= 4 * kLuThreads) hipLaunchKernelGGL((lu_half_kernel<4, kNB, kLuThreads>), g, t, 0, s, (int)N, K0, cend, A, piv, info);
+      else hipLaunchKernelGGL((lu_half_kernel<kPanelMaxM, kNB, kLuThreads>), g, t, 0, s, (int)N, K0, cend, A, piv, info);
+    } else {
+      const dim3 t(kBigThreads);
+      if (R <= 2 * kBigThreads) hipLaunchKernelGGL((lu_half_kernel<2, kBigNB, kBigThreads>), g, t, 0, s, (int)N, K0, cend, A, piv, info);
+      else if (R <= 4 * kBigThreads) hipLaunchKernelGGL((lu_half_kernel<4, kBigNB, kBigThreads>), g, t, 0, s, (int)N, K0, cend, A, piv, info);
+      else if (R <= 8 * kBigThreads) hipLaunchKernelGGL((lu_half_kernel<8, kBigNB, kBigThreads>), g, t, 0, s, (int)N, K0, cend, A, piv, info);
+      else hipLaunchKernelGGL((lu_half_kernel<kBigMaxM, kBigNB, kBigThreads>), g, t, 0, s, (int)N, K0, cend, A, piv, info);
+    }
+    IADMM_CHECK_LAUNCH();
+    return 0;
+  }
   if (N <= kPanelMaxM * kLuThreads) {
     for (int k0 = K0; k0 < cend; k0 += kNB) {
       const int R = (int)N - k0;

@@ -37,7 +37,7 @@ def _data(B, n, mi, me, seed):
 
 
 def _leaves(d, keys, dev, dtype):
-    return {k: d[k].to(dev, dtype).requires_grad_(k in keys) for k in d}
+    return {k: d[k].detach().to(dev, dtype).clone().requires_grad_(k in keys) for k in d}
 
 
 # n % 4 != 0 exercises the scalar column path of iadmm_bmv_t and the unvectorised iadmm_bger
