@@ -267,217 +267,6 @@ __global__ __launch_bounds__(NT, NT <= 256 ? 2 : 1) void lu_panel_kernel(int N, 
   }
 }
 
-// Fused factorization of one 64-column half [K0, cend) in ONE launch (r03; r02 launched every NB-wide
-// sub-panel and every in-block update separately: 7 launches per half at N <= 2048).  One workgroup
-// per instance; thread t owns the rows K0 + t + NT m of the half for the whole launch.  Per sub-panel
-// k0 = K0 + NB j: load it (rows >= k0) into registers and factor it exactly as lu_panel_kernel does
-// (same pivot rule and operation order), write it back, apply its interchanges to the half's other
-// columns, U = L11^-1 A on its rows right of it inside the half (kept in LDS too), then the rank-NB
-// update of the half's columns right of it, rows >= k0 + NB, one NT-row chunk at a time: the chunk's
-// multipliers are staged in LDS by their row owners and the chunk is updated cooperatively with
-// accesses contiguous along the columns (as lu_update_block_kernel).  Same arithmetic per element as
-// the unfused kernels: the factors are bitwise those of the r02 sequence.
-template <int M, int NB, int NT>
-__global__ __launch_bounds__(NT, NT <= 256 ? 2 : 1) void lu_half_kernel(int N, int K0, int cend, float* A, int* piv,
-                                                                        int* info) {
-  constexpr int NWV = NT / 64;
-  __shared__ float xrow[2][NB];
-  __shared__ float L11[NB][NB + 1];
-  __shared__ float rv[NWV];
-  __shared__ int ri[NWV + 1];
-  __shared__ int pvs[NB], prow[2 * NB], pcur[2 * NB], pcnt[1];
-  __shared__ float Us[NB][kBlk];        // U rows of the sub-panel, columns of the half (relative to K0)
-  __shared__ float Lc[NT][NB + 1];      // multipliers of one NT-row chunk
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const size_t b = blockIdx.x;
-  float* Ab = A + b * (size_t)N * N;
-  const int R0 = N - K0;
-  float a[M][NB];
-  for (int k0 = K0; k0 < cend; k0 += NB) {
-    const int nb = min(NB, cend - k0);
-    const int j0 = k0 - K0;                       // rows [K0, k0) of the half are final
-    const bool vec = nb == NB && (N % 4) == 0 && aligned16(Ab) && (NB % 4) == 0;
-#pragma unroll
-    for (int m = 0; m < M; ++m) {
-      const int rr = tid + NT * m;
-      const bool live = rr >= j0 && rr < R0;
-      const float* src = Ab + (size_t)(K0 + min(max(rr, j0), R0 - 1)) * N + k0;
-      if (vec) {
-#pragma unroll
-        for (int c4 = 0; c4 < NB; c4 += 4) {
-          const float4 v = *reinterpret_cast<const float4*>(src + c4);
-          a[m][c4] = v.x; a[m][c4 + 1] = v.y; a[m][c4 + 2] = v.z; a[m][c4 + 3] = v.w;
-        }
-      } else {
-#pragma unroll
-        for (int c = 0; c < NB; ++c) a[m][c] = c < nb ? src[c] : 0.f;
-      }
-      if (!live) {
-#pragma unroll
-        for (int c = 0; c < NB; ++c) a[m][c] = 0.f;
-      }
-    }
-#pragma unroll
-    for (int j = 0; j < NB; ++j) {
-      if (j < nb) {
-        const int jr = j0 + j;                    // row k0 + j, relative to K0: owned by thread jr, m = 0
-        float best = -1.f;
-        int bi = R0;
-#pragma unroll
-        for (int m = 0; m < M; ++m) {
-          const int rr = tid + NT * m;
-          const float v = fabsf(col_of(a[m], j));
-          if (rr >= jr && rr < R0 && v > best) { best = v; bi = rr; }
-        }
-#pragma unroll
-        for (int o = 32; o >= 1; o >>= 1) {
-          const float ov = __shfl_xor(best, o, 64);
-          const int oi = __shfl_xor(bi, o, 64);
-          if (ov > best || (ov == best && oi < bi)) { best = ov; bi = oi; }
-        }
-        if (lane == 0) { rv[wave] = best; ri[wave] = bi; }
-        if (tid == jr) {
-#pragma unroll
-          for (int c = 0; c < NB; ++c) xrow[0][c] = a[0][c];
-        }
-        __syncthreads();
-        if (tid == 0) {
-          float bv = rv[0];
-          int bx = ri[0];
-          for (int w = 1; w < NWV; ++w)
-            if (rv[w] > bv || (rv[w] == bv && ri[w] < bx)) { bv = rv[w]; bx = ri[w]; }
-          if (bx >= R0) bx = jr;  // all entries NaN: keep the diagonal
-          else if (bv == 0.f && info[b] == 0) info[b] = k0 + j + 1;
-          ri[NWV] = bx;
-          piv[b * N + k0 + j] = K0 + bx + 1;
-          pvs[j] = K0 + bx;
-        }
-        __syncthreads();
-        const int p = ri[NWV];
-#pragma unroll
-        for (int m = 0; m < M; ++m)
-          if (tid + NT * m == p) {
-#pragma unroll
-            for (int c = 0; c < NB; ++c) {
-              xrow[1][c] = a[m][c];
-              a[m][c] = xrow[0][c];
-            }
-          }
-        __syncthreads();
-        if (tid == jr) {
-#pragma unroll
-          for (int c = 0; c < NB; ++c) a[0][c] = xrow[1][c];
-        }
-        const float pv = xrow[1][j];
-        if (pv != 0.f) {
-          const float rcp = 1.0f / pv;
-          float pr[NB];
-#pragma unroll
-          for (int c = 0; c < NB; ++c) pr[c] = xrow[1][c];
-#pragma unroll
-          for (int m = 0; m < M; ++m) {
-            const int rr = tid + NT * m;
-            if (rr > jr && rr < R0) {
-              const float l = col_of(a[m], j) * rcp;
-#pragma unroll
-              for (int c = 0; c < NB; ++c) {
-                if (c == j) a[m][c] = l;
-                else if (c > j) a[m][c] = a[m][c] - l * pr[c];
-              }
-            }
-          }
-        }
-        __syncthreads();  // xrow is rewritten by the next column
-      }
-    }
-    // the factored sub-panel back to HBM; L11 for the substitution
-#pragma unroll
-    for (int m = 0; m < M; ++m) {
-      const int rr = tid + NT * m;
-      if (rr >= j0 && rr < R0) {
-        float* dst = Ab + (size_t)(K0 + rr) * N + k0;
-        if (vec) {
-#pragma unroll
-          for (int c4 = 0; c4 < NB; c4 += 4)
-            *reinterpret_cast<float4*>(dst + c4) = make_float4(a[m][c4], a[m][c4 + 1], a[m][c4 + 2], a[m][c4 + 3]);
-        } else {
-#pragma unroll
-          for (int c = 0; c < NB; ++c)
-            if (c < nb) dst[c] = a[m][c];
-        }
-      }
-    }
-    if (tid >= j0 && tid < j0 + nb) {
-#pragma unroll
-      for (int c = 0; c < NB; ++c) L11[tid - j0][c] = a[0][c];
-    }
-    // interchanges on the half's columns outside the sub-panel (lu_panel_kernel's ?laswp step)
-    build_row_perm(pvs, k0, nb, prow, pcur, pcnt);  // (its barrier also publishes L11 and the stores above)
-    {
-      const int cnt = *pcnt;
-      const int col = K0 + tid;
-      if (tid < kBlk && col < cend && (col < k0 || col >= k0 + nb)) {
-        float v[2 * NB];
-#pragma unroll
-        for (int i = 0; i < 2 * NB; ++i) v[i] = i < cnt ? Ab[(size_t)pcur[i] * N + col] : 0.f;
-#pragma unroll
-        for (int i = 0; i < 2 * NB; ++i)
-          if (i < cnt) Ab[(size_t)prow[i] * N + col] = v[i];
-      }
-    }
-    const int cr0 = k0 + nb;                      // first column right of the sub-panel
-    if (cr0 >= cend) break;                       // last sub-panel of the half: no update inside it
-    __syncthreads();
-    // U = L11^-1 A on the sub-panel rows, columns [cr0, cend) (one thread per column)
-    {
-      const int c = cr0 + tid;
-      if (tid < cend - cr0) {
-        float x[NB];
-#pragma unroll
-        for (int i = 0; i < NB; ++i) x[i] = i < nb ? Ab[(size_t)(k0 + i) * N + c] : 0.f;
-#pragma unroll
-        for (int i = 1; i < NB; ++i) {
-          float s = x[i];
-#pragma unroll
-          for (int l = 0; l < i; ++l) s = s - L11[i][l] * x[l];
-          x[i] = s;
-        }
-#pragma unroll
-        for (int i = 0; i < NB; ++i)
-          if (i < nb) {
-            Ab[(size_t)(k0 + i) * N + c] = x[i];
-            Us[i][c - K0] = x[i];
-          }
-      }
-    }
-    // rank-nb update of [cr0, cend) for the rows below the sub-panel, chunk by chunk
-    const int w = cend - cr0;
-#pragma unroll
-    for (int m = 0; m < M; ++m) {
-      const int rr = tid + NT * m;
-      __syncthreads();  // Us written / the previous chunk's Lc consumed
-#pragma unroll
-      for (int l = 0; l < NB; ++l) Lc[tid][l] = a[m][l];
-      __syncthreads();
-      const int rbeg = max(NT * m, j0 + nb), rend = min(NT * (m + 1), R0);
-      if (rbeg >= rend) continue;
-      const int rows = rend - rbeg, tot = rows * w;
-      (void)rr;
-      for (int idx = tid; idx < tot; idx += NT) {
-        const int r = idx / w, c = idx - r * w;
-        const int rl = rbeg + r;                  // row relative to K0
-        float* ap = Ab + (size_t)(K0 + rl) * N + cr0 + c;
-        float v = *ap;
-#pragma unroll
-        for (int l = 0; l < NB; ++l)
-          if (l < nb) v = v - Lc[rl - NT * m][l] * Us[l][cr0 - K0 + c];
-        *ap = v;
-      }
-    }
-    __syncthreads();  // the updated columns are re-read as the next sub-panel
-  }
-}
-
 // A[c0.., c0..cend) -= L21 U12 inside the current 64-column block, c0 = k0 + 16: rows
 // [c0 + blockIdx.y*64, +64) of instance blockIdx.x, w = cend - c0 <= 64 - NB columns.
 template <int NB>
@@ -513,52 +302,55 @@ __global__ __launch_bounds__(256) void lu_update_block_kernel(int N, int k0, int
   }
 }
 
-// Once per 64-column block [K0, cend): the net row permutation of its interchanges, one wave per
-// instance, into perm[b] = {rowid[128], cur[128], cnt} (kPermInts ints).
-constexpr int kPermInts = 4 * kBlk + 1;
+// The net row permutation of the interchanges of rows [K0, cend) (a 64-column half or, composed, a
+// whole 128-column block: nbk <= 128), one wave per instance, into perm[b] = {rowid[256], cur[256],
+// cnt} (kPermInts ints).
+constexpr int kPermMax = 128;
+constexpr int kPermInts = 4 * kPermMax + 1;
 __global__ __launch_bounds__(64) void lu_block_perm_kernel(int N, int K0, int cend, const int* piv, int* perm) {
-  __shared__ int pvs[kBlk], prow[2 * kBlk], pcur[2 * kBlk], pcnt[1];
+  __shared__ int pvs[kPermMax], prow[2 * kPermMax], pcur[2 * kPermMax], pcnt[1];
   const int tid = threadIdx.x, nbk = cend - K0;
   const size_t b = blockIdx.x;
-  if (tid < nbk) pvs[tid] = piv[b * N + K0 + tid] - 1;
+  for (int i = tid; i < nbk; i += 64) pvs[i] = piv[b * N + K0 + i] - 1;
   __syncthreads();
   build_row_perm(pvs, K0, nbk, prow, pcur, pcnt);
   int* out = perm + b * kPermInts;
-  for (int i = tid; i < 2 * kBlk; i += 64) { out[i] = prow[i]; out[2 * kBlk + i] = pcur[i]; }
-  if (tid == 0) out[4 * kBlk] = *pcnt;
+  for (int i = tid; i < 2 * kPermMax; i += 64) { out[i] = prow[i]; out[2 * kPermMax + i] = pcur[i]; }
+  if (tid == 0) out[4 * kPermMax] = *pcnt;
 }
 
-// Once per block: its row interchanges on the columns outside it (the final L left of it, A12 /
-// A22 right of it), and for the right columns [cend, trsm_end) U12 = L11^-1 A12 on the block rows (L11 = the
-// block's unit-lower multipliers, in LDS, broadcast reads).  One thread per column.  Every row
-// outside the block that the interchanges touch ends up holding an original block row, so: the
-// new block rows are loaded first (x, registers), then the outside rows are moved 16 at a time
-// (their sources are block rows, which are only stored to afterwards), then the substitution and
-// the block-row stores.  Column index space: [0, K0) then [cend, N).
-__global__ __launch_bounds__(256) void lu_swap_trsm_block_kernel(int N, int K0, int cend, int trsm_end, float* A,
-                                                                 const int* perm) {
-  __shared__ float Ld[kBlk][kBlk + 1];
-  __shared__ int prow[2 * kBlk], pcur[2 * kBlk], pcnt[1];
+// The row interchanges of rows [K0, K0 + nbk) (perm from lu_block_perm_kernel, nbk <= NBK) on the
+// columns [a0, a1) and [b0, b1) (one thread per column), and for the columns [b0, trsm_end) (TRSM:
+// NBK == nbk == 64) U12 = L11^-1 A12 on the block rows (L11 = the block's unit-lower multipliers, in
+// LDS, broadcast reads).  Every row outside the block that the interchanges touch ends up holding
+// an original block row, so: the new block rows are loaded first (x, registers), then the outside
+// rows are moved 16 at a time (their sources are block rows, which are only stored to afterwards),
+// then the substitution and the block-row stores.
+template <int NBK, bool TRSM>
+__global__ __launch_bounds__(256) void lu_swap_kernel(int N, int K0, int nbk, int a0, int a1, int b0, int b1,
+                                                      int trsm_end, float* A, const int* perm) {
+  __shared__ float Ld[TRSM ? kBlk : 1][kBlk + 1];
+  __shared__ int prow[2 * kPermMax], pcur[2 * kPermMax], pcnt[1];
   const int tid = threadIdx.x;
   const size_t b = blockIdx.x;
   float* Ab = A + b * (size_t)N * N;
-  const int nbk = cend - K0;
-  if (trsm_end > cend)
+  if constexpr (TRSM) {
     for (int idx = tid; idx < kBlk * kBlk; idx += blockDim.x) {
       const int r = idx / kBlk, c = idx % kBlk;
       Ld[r][c] = Ab[(size_t)(K0 + r) * N + K0 + c];
     }
+  }
   const int* pb = perm + b * kPermInts;
-  if (tid < 2 * kBlk) { prow[tid] = pb[tid]; pcur[tid] = pb[2 * kBlk + tid]; }
-  if (tid == 0) *pcnt = pb[4 * kBlk];
+  for (int i = tid; i < 2 * kPermMax; i += blockDim.x) { prow[i] = pb[i]; pcur[i] = pb[2 * kPermMax + i]; }
+  if (tid == 0) *pcnt = pb[4 * kPermMax];
   __syncthreads();
   const int cnt = *pcnt;
-  const int q = blockIdx.y * blockDim.x + tid;
-  const int c = q < K0 ? q : cend + (q - K0);
-  if (c >= N) return;
-  float x[kBlk];
+  const int q = blockIdx.y * blockDim.x + tid, na = a1 - a0;
+  const int c = q < na ? a0 + q : b0 + (q - na);
+  if (q >= na && c >= b1) return;
+  float x[NBK];
 #pragma unroll
-  for (int i = 0; i < kBlk; ++i) x[i] = i < nbk ? Ab[(size_t)pcur[i] * N + c] : 0.f;
+  for (int i = 0; i < NBK; ++i) x[i] = i < nbk ? Ab[(size_t)pcur[i] * N + c] : 0.f;
   for (int i0 = nbk; i0 < cnt; i0 += 16) {
     float y[16];
 #pragma unroll
@@ -567,17 +359,19 @@ __global__ __launch_bounds__(256) void lu_swap_trsm_block_kernel(int N, int K0, 
     for (int i = 0; i < 16; ++i)
       if (i0 + i < cnt) Ab[(size_t)prow[i0 + i] * N + c] = y[i];
   }
-  if (c >= cend && c < trsm_end) {  // right of the block (nbk == kBlk): U12 = L11^-1 A12 where asked
+  if constexpr (TRSM) {
+    if (q >= na && c < trsm_end) {
 #pragma unroll
-    for (int i = 1; i < kBlk; ++i) {
-      float s = x[i];
+      for (int i = 1; i < kBlk; ++i) {
+        float s = x[i];
 #pragma unroll
-      for (int l = 0; l < i; ++l) s = s - Ld[i][l] * x[l];
-      x[i] = s;
+        for (int l = 0; l < i; ++l) s = s - Ld[i][l] * x[l];
+        x[i] = s;
+      }
     }
   }
 #pragma unroll
-  for (int i = 0; i < kBlk; ++i)
+  for (int i = 0; i < NBK; ++i)
     if (i < nbk) Ab[(size_t)(K0 + i) * N + c] = x[i];
 }
 
@@ -753,36 +547,39 @@ static_assert(kT2S * kT2K + kT2S * kT2CS >= kOB * kT2K, "L11^-1 staging must fit
 static_assert(kT2Lds <= 160 * 1024, "gfx950 LDS");
 constexpr int kLinvFloats = kOB * kOB;
 
-// Linv[b] = (unit lower part of A[P:P+128, P:P+128])^-1, row-major 128 x 128.  Column j of the inverse
-// (thread j) by forward substitution x_i = -sum_{j<=k<i} L_ik x_k, x_j = 1, with L and X in LDS.
+// Linv[b] = (unit lower part of A[P:P+128, P:P+128])^-1, row-major 128 x 128.  Thread j computes
+// column j by forward substitution x_i = -sum_{k<i} L_ik x_k (x_k = 0 for k < j, x_j = 1) with the
+// column in registers (both loops unrolled) and L broadcast from LDS 4 entries per read; four
+// partial sums per row shorten the dependent chains.  (r03 first form: L and X both in LDS, one
+// workgroup per CU, LDS-latency bound: 1.6 ms per block at B = 1024, 15x this one.)
 __global__ __launch_bounds__(kOB) void lu_linv_kernel(int N, int P, const float* A, float* Linv) {
-  __shared__ float L[kOB][kOB + 1];
-  __shared__ float X[kOB][kOB + 1];
-  const int tid = threadIdx.x;
+  __shared__ __attribute__((aligned(16))) float L[kOB][kOB + 4];
+  const int j = threadIdx.x;
   const size_t b = blockIdx.x;
   const float* Ab = A + b * (size_t)N * N;
-  for (int idx = tid; idx < kOB * kOB; idx += blockDim.x) {
+  for (int idx = j; idx < kOB * kOB; idx += blockDim.x) {
     const int r = idx / kOB, c = idx % kOB;
     L[r][c] = c < r ? Ab[(size_t)(P + r) * N + P + c] : 0.f;
   }
   __syncthreads();
-  const int j = tid;
+  float x[kOB];
+#pragma unroll
   for (int i = 0; i < kOB; ++i) {
-    float v;
-    if (i < j) {
-      v = 0.f;
-    } else if (i == j) {
-      v = 1.f;
-    } else {
-      v = 0.f;
-      for (int k = j; k < i; ++k) v = fmaf(L[i][k], X[k][j], v);
-      v = -v;
+    float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+#pragma unroll
+    for (int k4 = 0; k4 < (i & ~3); k4 += 4) {
+      const float4 l = *reinterpret_cast<const float4*>(&L[i][k4]);
+      s0 = fmaf(l.x, x[k4], s0); s1 = fmaf(l.y, x[k4 + 1], s1);
+      s2 = fmaf(l.z, x[k4 + 2], s2); s3 = fmaf(l.w, x[k4 + 3], s3);
     }
-    X[i][j] = v;
+#pragma unroll
+    for (int k = i & ~3; k < i; ++k) s0 = fmaf(L[i][k], x[k], s0);
+    const float v = -((s0 + s1) + (s2 + s3));
+    x[i] = i < j ? 0.f : (i == j ? 1.f : v);
   }
-  __syncthreads();
   float* out = Linv + b * (size_t)kLinvFloats;
-  for (int idx = tid; idx < kOB * kOB; idx += blockDim.x) out[idx] = X[idx / kOB][idx % kOB];
+#pragma unroll
+  for (int i = 0; i < kOB; ++i) out[i * kOB + j] = x[i];
 }
 
 // Fused U12 = L11^-1 A12 and A22 -= L21 U12 (rank 128) for the columns right of [P, P + 128).  One
@@ -794,7 +591,8 @@ __global__ __launch_bounds__(kOB) void lu_linv_kernel(int N, int P, const float*
 //             (wr, wc) owns 32 x 32 of a step (v_mfma_f32_32x32x2f32, 64 per step: lane half h covers
 //             k in [64h, 64h + 64)).
 // Strips of one instance are consecutive logical ids on one XCD (its L2 serves the L21 re-reads).
-template <bool VEC>
+// DIAG (tools/lubench128.hip only): 1 = no MFMAs in the main loop, 2 = no global A22 / L21 traffic in it.
+template <bool VEC, int DIAG = 0>
 __global__ __launch_bounds__(kT2Threads, 1) void lu_trail128_kernel(int N, int P, int ntc, float* A,
                                                                     const float* Linv) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
@@ -882,7 +680,10 @@ __global__ __launch_bounds__(kT2Threads, 1) void lu_trail128_kernel(int N, int P
     }
   }
 
-  // ---- main loop: A22 -= L21 U12
+  // ---- main loop: A22 -= L21 U12.  Per step: the product L21 U12 from zero on MFMA, then
+  // out = A22 - product where the A22 values are already in registers (each thread stores exactly
+  // the elements it prefetched), so A22 never passes through LDS on the way in: two barriers per
+  // step, the next step's A22 / L21 loads in flight during the MFMAs.
   const int wr = (wave >> 2) * 32, wc = (wave & 3) * 32;
   auto loadC = [&](int step, VT (&c)[kCQ]) {
 #pragma unroll
@@ -898,59 +699,68 @@ __global__ __launch_bounds__(kT2Threads, 1) void lu_trail128_kernel(int N, int P
       l[q] = ld(min(row, N - 1), P + (e % LPR) * W, row < N);
     }
   };
-  auto writeCL = [&](const VT (&c)[kCQ], const VT (&l)[kLQ]) {
-#pragma unroll
-    for (int q = 0; q < kCQ; ++q) {
-      const int e = tid + NT * q;
-      st_lds(Cb + (e / CPR) * kT2CS + (e % CPR) * W, c[q], 1.f);
-    }
+  auto writeL = [&](const VT (&l)[kLQ]) {
 #pragma unroll
     for (int q = 0; q < kLQ; ++q) {
       const int e = tid + NT * q;
-      st_lds(Ls + (e / LPR) * kT2K + (e % LPR) * W, l[q], -1.f);
+      st_lds(Ls + (e / LPR) * kT2K + (e % LPR) * W, l[q], 1.f);
     }
   };
-  auto storeOut = [&](int step) {
+  auto storeOut = [&](int step, const VT (&c)[kCQ]) {
 #pragma unroll
     for (int q = 0; q < kCQ; ++q) {
       const int e = tid + NT * q, row = c0 + step * kT2S + e / CPR, col = cb + (e % CPR) * W;
       if (row < N && col < N) {
         const float* src = Cb + (e / CPR) * kT2CS + (e % CPR) * W;
-        if constexpr (VEC) *reinterpret_cast<float4*>(Ab + (size_t)row * N + col) = *reinterpret_cast<const float4*>(src);
-        else Ab[(size_t)row * N + col] = *src;
+        if constexpr (VEC) {
+          const float4 pr = *reinterpret_cast<const float4*>(src);
+          *reinterpret_cast<float4*>(Ab + (size_t)row * N + col) =
+              make_float4(c[q].x - pr.x, c[q].y - pr.y, c[q].z - pr.z, c[q].w - pr.w);
+        } else {
+          Ab[(size_t)row * N + col] = c[q] - *src;
+        }
       }
     }
   };
 
-  VT cr[kCQ], lr[kLQ];
-  loadC(0, cr);
-  loadL(0, lr);
-  writeCL(cr, lr);  // Ls / Cb: the prologue's last reads of Li finished before the barrier above
-  __syncthreads();
-  for (int step = 0; step < nsteps; ++step) {
+  // A22 of step s + 1 and L21 of step s + 2 are loaded during step s (two register sets each,
+  // alternating roles: the loop is unrolled by two so no register copy waits on a load): L21 goes to
+  // LDS in the middle of step s + 1, a step and a half after its loads were issued.
+  auto body = [&](int step, VT (&cc)[kCQ], VT (&cn)[kCQ], const VT (&lw)[kLQ], VT (&lnext)[kLQ]) {
     const bool more = step + 1 < nsteps;
+    if (more && DIAG != 2) {
+      loadC(step + 1, cn);
+      if (step + 2 < nsteps) loadL(step + 2, lnext);
+    }
     floatx16 acc;
 #pragma unroll
-    for (int v = 0; v < 16; ++v) acc[v] = Cb[(wr + 8 * (v >> 2) + 4 * h + (v & 3)) * kT2CS + wc + il];
-    if (more) {
-      loadC(step + 1, cr);
-      loadL(step + 1, lr);
-    }
+    for (int v = 0; v < 16; ++v) acc[v] = 0.f;
+    if constexpr (DIAG != 1) {
 #pragma unroll 4
-    for (int sg = 0; sg < kOB / 8; ++sg) {
-      const float4 fa = *reinterpret_cast<const float4*>(Ls + (wr + il) * kT2K + (kOB / 2) * h + 4 * sg);
-      const float4 fb = *reinterpret_cast<const float4*>(Ut + (wc + il) * kT2K + (kOB / 2) * h + 4 * sg);
+      for (int sg = 0; sg < kOB / 8; ++sg) {
+        const float4 fa = *reinterpret_cast<const float4*>(Ls + (wr + il) * kT2K + (kOB / 2) * h + 4 * sg);
+        const float4 fb = *reinterpret_cast<const float4*>(Ut + (wc + il) * kT2K + (kOB / 2) * h + 4 * sg);
 #pragma unroll
-      for (int s4 = 0; s4 < 4; ++s4) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(get4(fa, s4), get4(fb, s4), acc, 0, 0, 0);
+        for (int s4 = 0; s4 < 4; ++s4) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(get4(fa, s4), get4(fb, s4), acc, 0, 0, 0);
+      }
     }
-    __syncthreads();  // Cb (this step's A22) and Ls consumed by every wave
+    __syncthreads();  // Ls consumed by every wave; the previous step's Cb reads are done
 #pragma unroll
     for (int v = 0; v < 16; ++v) Cb[(wr + 8 * (v >> 2) + 4 * h + (v & 3)) * kT2CS + wc + il] = acc[v];
-    __syncthreads();
-    storeOut(step);
-    __syncthreads();  // Cb drained
-    if (more) writeCL(cr, lr);
-    __syncthreads();
+    if (more) writeL(lw);
+    __syncthreads();  // Cb holds this step's product, Ls the next step's L21
+    if (DIAG != 2) storeOut(step, cc);
+  };
+
+  VT c0r[kCQ], c1r[kCQ], la[kLQ], lb[kLQ];
+  loadC(0, c0r);
+  loadL(0, la);
+  if (nsteps > 1) loadL(1, lb);
+  writeL(la);  // Ls: the prologue's last reads of Li finished before the barrier above
+  __syncthreads();
+  for (int step = 0; step < nsteps; step += 2) {
+    body(step, c0r, c1r, lb, la);
+    if (step + 1 < nsteps) body(step + 1, c1r, c0r, la, lb);
   }
 }
 
@@ -1079,31 +889,8 @@ __global__ void kkt_rhs_kernel(int64_t B, int n, int m, int num_ineq, const floa
 
 using namespace iadmm;
 
-#ifndef IADMM_LU_FUSED_HALF
-#define IADMM_LU_FUSED_HALF 1   // 0: one launch per sub-panel and per in-block update (r02; tools A/B only)
-#endif
-
 // Panels (+ in-block updates) of the 64-column half [K0, cend).
 static int lu_factor_half(int64_t B, int64_t N, int K0, int cend, float* A, int* piv, int* info, hipStream_t s) {
-  if (IADMM_LU_FUSED_HALF) {
-    const int R = (int)N - K0;
-    const dim3 g((unsigned)B);
-    if (N <= kPanelMaxM * kLuThreads) {
-      const dim3 t(kLuThreads);
-      if (R <= kLuThreads) hipLaunchKernelGGL((lu_half_kernel<1, kNB, kLuThreads>), g, t, 0, s, (int)N, K0, cend, A, piv, info);
-      else if (R <= 2 * kLuThreads) hipLaunchKernelGGL((lu_half_kernel<2, kNB, kLuThreads>), g, t, 0, s, (int)N, K0, cend, A, piv, info);
-      else if (R <= 4 * kLuThreads) hipLaunchKernelGGL((lu_half_kernel<4, kNB, kLuThreads>), g, t, 0, s, (int)N, K0, cend, A, piv, info);
-      else hipLaunchKernelGGL((lu_half_kernel<kPanelMaxM, kNB, kLuThreads>), g, t, 0, s, (int)N, K0, cend, A, piv, info);
-    } else {
-      const dim3 t(kBigThreads);
-      if (R <= 2 * kBigThreads) hipLaunchKernelGGL((lu_half_kernel<2, kBigNB, kBigThreads>), g, t, 0, s, (int)N, K0, cend, A, piv, info);
-      else if (R <= 4 * kBigThreads) hipLaunchKernelGGL((lu_half_kernel<4, kBigNB, kBigThreads>), g, t, 0, s, (int)N, K0, cend, A, piv, info);
-      else if (R <= 8 * kBigThreads) hipLaunchKernelGGL((lu_half_kernel<8, kBigNB, kBigThreads>), g, t, 0, s, (int)N, K0, cend, A, piv, info);
-      else hipLaunchKernelGGL((lu_half_kernel<kBigMaxM, kBigNB, kBigThreads>), g, t, 0, s, (int)N, K0, cend, A, piv, info);
-    }
-    IADMM_CHECK_LAUNCH();
-    return 0;
-  }
   if (N <= kPanelMaxM * kLuThreads) {
     for (int k0 = K0; k0 < cend; k0 += kNB) {
       const int R = (int)N - k0;
@@ -1140,16 +927,23 @@ static int lu_factor_half(int64_t B, int64_t N, int K0, int cend, float* A, int*
   return 0;
 }
 
-// The half's row interchanges on every column outside [K0, cend), with U12 = L11^-1 A12 for the
-// columns [cend, trsm_end).
-static int lu_swap_half(int64_t B, int64_t N, int K0, int cend, int trsm_end, float* A, const int* piv, int* perm,
-                        hipStream_t s) {
-  const int outside = K0 + ((int)N - cend);
-  if (outside <= 0) return 0;
+// The interchanges of rows [K0, cend) (cend - K0 <= 128) on the columns [a0, a1) and [b0, b1), with
+// U12 = L11^-1 A12 for the columns [b0, trsm_end) (a 64-row half only).
+static int lu_swap(int64_t B, int64_t N, int K0, int cend, int a0, int a1, int b0, int b1, int trsm_end, float* A,
+                   const int* piv, int* perm, hipStream_t s) {
+  a1 = std::max(a0, a1);
+  b1 = std::max(b0, b1);
+  const int cols = (a1 - a0) + (b1 - b0), nbk = cend - K0;
+  if (cols <= 0 || nbk <= 0) return 0;
   hipLaunchKernelGGL(lu_block_perm_kernel, dim3((unsigned)B), dim3(64), 0, s, (int)N, K0, cend, piv, perm);
   IADMM_CHECK_LAUNCH();
-  hipLaunchKernelGGL(lu_swap_trsm_block_kernel, dim3((unsigned)B, (unsigned)((outside + 255) / 256)), dim3(256), 0, s,
-                     (int)N, K0, cend, trsm_end, A, perm);
+  const dim3 grid((unsigned)B, (unsigned)((cols + 255) / 256));
+  if (trsm_end > b0)
+    hipLaunchKernelGGL((lu_swap_kernel<kBlk, true>), grid, dim3(256), 0, s, (int)N, K0, nbk, a0, a1, b0, b1, trsm_end, A, perm);
+  else if (nbk <= kBlk)
+    hipLaunchKernelGGL((lu_swap_kernel<kBlk, false>), grid, dim3(256), 0, s, (int)N, K0, nbk, a0, a1, b0, b1, 0, A, perm);
+  else
+    hipLaunchKernelGGL((lu_swap_kernel<kPermMax, false>), grid, dim3(256), 0, s, (int)N, K0, nbk, a0, a1, b0, b1, 0, A, perm);
   IADMM_CHECK_LAUNCH();
   return 0;
 }
@@ -1182,23 +976,25 @@ static int lu_factor_blocks(int64_t B, int64_t N, float* A, int* piv, int* info,
     for (int K0 = 0; K0 < N && !rc; K0 += kBlk) {
       const int cend = (int)std::min<int64_t>(N, K0 + kBlk);
       rc = lu_factor_half(B, N, K0, cend, A, piv, info, s);
-      if (!rc) rc = lu_swap_half(B, N, K0, cend, (int)N, A, piv, perm, s);
+      if (!rc) rc = lu_swap(B, N, K0, cend, 0, K0, cend, (int)N, (int)N, A, piv, perm, s);
       if (!rc) rc = lu_rank64(B, N, K0, cend, (int)N, A, vec, s);
     }
     return rc;
   }
   for (int P = 0; P < N && !rc; P += kOB) {
-    const int c1 = (int)std::min<int64_t>(N, P + kBlk), c2 = (int)std::min<int64_t>(N, P + kOB);
-    // first half: factor, interchanges everywhere else, U12 for the second half's columns only, and
-    // the second half's rank-64 update
+    const int n_ = (int)N;
+    const int c1 = std::min(n_, P + kBlk), c2 = std::min(n_, P + kOB);
+    // first half: factor; its interchanges and U12 on the second half's columns only, then the second
+    // half's rank-64 update
     rc = lu_factor_half(B, N, P, c1, A, piv, info, s);
-    if (!rc) rc = lu_swap_half(B, N, P, c1, c2, A, piv, perm, s);
+    if (!rc && c1 < n_) rc = lu_swap(B, N, P, c1, 0, 0, c1, c2, c2, A, piv, perm, s);
     if (!rc) rc = lu_rank64(B, N, P, c1, c2, A, vec, s);
-    if (rc || c1 >= N) break;
-    // second half: factor, interchanges everywhere else (no substitution)
-    rc = lu_factor_half(B, N, c1, c2, A, piv, info, s);
-    if (!rc) rc = lu_swap_half(B, N, c1, c2, c2, A, piv, perm, s);
-    if (rc || c2 >= N) break;
+    // second half: factor; its interchanges on the first half's columns
+    if (!rc && c1 < n_) rc = lu_factor_half(B, N, c1, c2, A, piv, info, s);
+    if (!rc && c1 < n_) rc = lu_swap(B, N, c1, c2, P, c1, 0, 0, 0, A, piv, perm, s);
+    // the whole block's interchanges (composed) on the columns left and right of it, in one pass
+    if (!rc) rc = lu_swap(B, N, P, c2, 0, P, c2, n_, 0, A, piv, perm, s);
+    if (rc || c2 >= n_) break;
     // U12 = L11^-1 A12 and the rank-128 update of everything right of the block
     hipLaunchKernelGGL(lu_linv_kernel, dim3((unsigned)B), dim3(kOB), 0, s, (int)N, P, A, linv);
     IADMM_CHECK_LAUNCH();

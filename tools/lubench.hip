@@ -22,10 +22,10 @@ float run(int B, int N, int K0, float* A, int reps) {
   CK(hipFuncSetAttribute((const void*)lu_trail_kernel<true, DIAG>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kTrailLds));
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
-  hipLaunchKernelGGL((lu_trail_kernel<true, DIAG>), dim3(B * ntc * nrc), dim3(kTrailThreads), kTrailLds, 0, N, K0, ntc, nrc, A);
+  hipLaunchKernelGGL((lu_trail_kernel<true, DIAG>), dim3(B * ntc * nrc), dim3(kTrailThreads), kTrailLds, 0, N, K0, ntc, nrc, N, A);
   CK(hipEventRecord(e0));
   for (int r = 0; r < reps; ++r)
-    hipLaunchKernelGGL((lu_trail_kernel<true, DIAG>), dim3(B * ntc * nrc), dim3(kTrailThreads), kTrailLds, 0, N, K0, ntc, nrc, A);
+    hipLaunchKernelGGL((lu_trail_kernel<true, DIAG>), dim3(B * ntc * nrc), dim3(kTrailThreads), kTrailLds, 0, N, K0, ntc, nrc, N, A);
   CK(hipEventRecord(e1));
   CK(hipEventSynchronize(e1));
   float ms;
