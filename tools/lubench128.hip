@@ -48,7 +48,7 @@ int main(int argc, char** argv) {
     for (int round = 0; round < 2; ++round) {
       float t[3] = {run<0>(B, N, P, A, Linv, 5), run<1>(B, N, P, A, Linv, 5), run<2>(B, N, P, A, Linv, 5)};
       for (int v = 0; v < 3; ++v)
-        printf("P=%4d %-10s %8.3f ms  %7.0f GB/s alg  %6.1f TF\n", P, names[v], t[v], bytes / t[v] / 1e6, flops / t[v] / 1e9);
+        printf("P=%4d %-12s %8.3f ms  %7.0f GB/s alg  %6.1f TF\n", P, names[v], t[v], bytes / t[v] / 1e6, flops / t[v] / 1e9);
     }
   }
   CK(hipFree(A)); CK(hipFree(Linv));
