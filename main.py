@@ -58,6 +58,8 @@ def build_parser():
     add("--data_dir", type=str, default="./datasets")
     add("--micro_batch", type=int, default=0, help="instances per forward/backward pass (memory)")
     add("--max_minutes", type=float, default=0.0, help="train: stop after the epoch that exceeds this wall time")
+    add("--resume", type=str, default="", help="train: state file (model, Adam, epoch, EarlyStopping) written after "
+                                               "every epoch and continued from when it exists")
     return p
 
 
@@ -330,7 +332,16 @@ def run_train(args):
     packed = solver.PackedWeights()
     history = []
     t_start = time.time()
-    for epoch in range(args.num_epoch):
+    first_epoch = 0
+    if args.resume and os.path.exists(args.resume):  # this repo's own state file (tensors + scalars only)
+        st = torch.load(args.resume, map_location=device, weights_only=True)
+        model.load_state_dict(st["model"])
+        optimizer.load_state_dict(st["optimizer"])
+        stopper.best_loss, stopper.counter = st["best_loss"], int(st["counter"])
+        first_epoch = int(st["epoch"]) + 1
+        if rank == 0:
+            print(f"[train] resumed from {args.resume} after epoch {first_epoch - 1}", file=sys.stderr, flush=True)
+    for epoch in range(first_epoch, args.num_epoch):
         model.train()
         t0 = time.time()
         loss = float("nan")
@@ -390,6 +401,9 @@ def run_train(args):
             dist.broadcast(flag, 0)
             stop = bool(flag.item())
         history.append((loss, val_obj))
+        if args.resume and rank == 0:
+            torch.save({"model": model.state_dict(), "optimizer": optimizer.state_dict(), "epoch": epoch,
+                        "best_loss": stopper.best_loss, "counter": stopper.counter}, args.resume)
         if stop:
             break
     if dist is not None:
