@@ -39,6 +39,7 @@ constexpr int kPanelMaxM = 8;      // panel rows per thread: N <= 8 * 256 (12 ro
 constexpr int kBigNB = 8;          // panel width above N = 8 * 256
 constexpr int kBigThreads = 1024;  // panel workgroup size above N = 8 * 256
 constexpr int kBigMaxM = 10;       // rows per thread there: N <= 10 * 1024 (12 spills at 128 VGPRs)
+constexpr int kLuMaxN = 36736;     // = lu_solve's LDS limit; panels past 10240 rows run from HBM
 constexpr int kLuThreads = 256;
 constexpr int kUpdRows = 64;
 constexpr int kSolveBlk = 64;
@@ -91,6 +92,48 @@ IADMM_DEV float col_of(const float (&row)[NB], int j) {  // row[j] for a run-tim
 #pragma unroll
   for (int c = 1; c < NB; ++c) v = c == j ? row[c] : v;
   return v;
+}
+
+// After a panel [k0, k0 + nb) is factored (L11 in LDS, its interchanges in pvs): the row
+// interchanges (?laswp) on the columns of the current 64-column block outside the panel (the
+// columns left and right of the block get the whole block's interchanges at once in
+// lu_swap_kernel), then U = L11^-1 A on the panel rows for the columns [k0 + nb, cend) of the block
+// (unit lower forward substitution, one column per thread with its loads issued before the
+// substitution).
+template <int NB>
+IADMM_DEV void panel_finish(float* Ab, int N, int K0, int k0, int nb, int cend, float (*L11)[NB + 1], const int* pvs,
+                            int* prow, int* pcur, int* pcnt) {
+  const int tid = threadIdx.x;
+  build_row_perm(pvs, k0, nb, prow, pcur, pcnt);  // (its barrier also publishes L11)
+  {
+    const int cnt = *pcnt;
+    const int col = K0 + tid;
+    if (col < cend && (col < k0 || col >= k0 + nb)) {
+      float v[2 * NB];
+#pragma unroll
+      for (int i = 0; i < 2 * NB; ++i) v[i] = i < cnt ? Ab[(size_t)pcur[i] * N + col] : 0.f;
+#pragma unroll
+      for (int i = 0; i < 2 * NB; ++i)
+        if (i < cnt) Ab[(size_t)prow[i] * N + col] = v[i];
+    }
+  }
+  __syncthreads();  // the substitution's column owners differ from the interchanges'
+  const int c = k0 + nb + tid;
+  if (c < cend) {
+    float x[NB];
+#pragma unroll
+    for (int i = 0; i < NB; ++i) x[i] = i < nb ? Ab[(size_t)(k0 + i) * N + c] : 0.f;
+#pragma unroll
+    for (int i = 1; i < NB; ++i) {
+      float s = x[i];
+#pragma unroll
+      for (int l = 0; l < i; ++l) s = s - L11[i][l] * x[l];
+      x[i] = s;
+    }
+#pragma unroll
+    for (int i = 0; i < NB; ++i)
+      if (i < nb) Ab[(size_t)(k0 + i) * N + c] = x[i];
+  }
 }
 
 // Panel shapes: <M, 16, 256> (2 workgroups per CU) for N <= 8 * 256 = 2048; above that
@@ -230,41 +273,80 @@ __global__ __launch_bounds__(NT, NT <= 256 ? 2 : 1) void lu_panel_kernel(int N, 
 #pragma unroll
     for (int c = 0; c < kNB; ++c) L11[tid][c] = a[0][c];
   }
-  // Row interchanges (?laswp) on the columns of the current 64-column block outside the panel
-  // (the columns left and right of the block get the whole block's interchanges at once in
-  // lu_swap_trsm_block_kernel), then U = L11^-1 A on the panel rows for the columns
-  // [k0 + nb, cend) of the block (unit lower forward substitution, one column per thread with
-  // its 16 loads issued before the substitution).
-  build_row_perm(pvs, k0, nb, prow, pcur, pcnt);  // (its barrier also publishes L11)
-  {
-    const int cnt = *pcnt;
-    const int col = K0 + tid;
-    if (col < cend && (col < k0 || col >= k0 + nb)) {
-      float v[2 * kNB];
-#pragma unroll
-      for (int i = 0; i < 2 * kNB; ++i) v[i] = i < cnt ? Ab[(size_t)pcur[i] * N + col] : 0.f;
-#pragma unroll
-      for (int i = 0; i < 2 * kNB; ++i)
-        if (i < cnt) Ab[(size_t)prow[i] * N + col] = v[i];
-    }
-  }
-  __syncthreads();  // the substitution's column owners differ from the interchanges'
-  const int c = k0 + nb + tid;
-  if (c < cend) {
-    float x[kNB];
-#pragma unroll
-    for (int i = 0; i < kNB; ++i) x[i] = i < nb ? Ab[(size_t)(k0 + i) * N + c] : 0.f;
-#pragma unroll
-    for (int i = 1; i < kNB; ++i) {
-      float s = x[i];
-#pragma unroll
-      for (int l = 0; l < i; ++l) s = s - L11[i][l] * x[l];
-      x[i] = s;
+  panel_finish<kNB>(Ab, N, K0, k0, nb, cend, L11, pvs, prow, pcur, pcnt);
+}
+
+// Global-memory panel for N > 10240 (rows beyond what the register panel can hold, up to the
+// solve's N <= 36736): the same column steps as lu_panel_kernel with the NB-wide panel in HBM /
+// L2 instead of registers (thread t owns rows k0 + t + NT i); the pivot row exchange and the
+// rank-1 update read and write the panel in place, a workgroup-wide barrier between the steps.
+// Same pivot rule (first max |a|) and operation order per element as the register panel.
+template <int NB, int NT>
+__global__ __launch_bounds__(NT, 1) void lu_panel_global_kernel(int N, int K0, int k0, int cend, float* A, int* piv,
+                                                                int* info) {
+  constexpr int NWV = NT / 64;
+  __shared__ float prw[NB];
+  __shared__ float L11[NB][NB + 1];
+  __shared__ float rv[NWV];
+  __shared__ int ri[NWV + 1];
+  __shared__ int pvs[NB], prow[2 * NB], pcur[2 * NB], pcnt[1];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const size_t b = blockIdx.x;
+  float* Ab = A + b * (size_t)N * N;
+  const int nb = min(NB, min(N - k0, cend - k0));
+  for (int j = 0; j < nb; ++j) {
+    const int c = k0 + j;
+    float best = -1.f;
+    int bi = N;
+    for (int r = c + tid; r < N; r += NT) {
+      const float v = fabsf(Ab[(size_t)r * N + c]);
+      if (v > best) { best = v; bi = r; }
     }
 #pragma unroll
-    for (int i = 0; i < kNB; ++i)
-      if (i < nb) Ab[(size_t)(k0 + i) * N + c] = x[i];
+    for (int o = 32; o >= 1; o >>= 1) {
+      const float ov = __shfl_xor(best, o, 64);
+      const int oi = __shfl_xor(bi, o, 64);
+      if (ov > best || (ov == best && oi < bi)) { best = ov; bi = oi; }
+    }
+    if (lane == 0) { rv[wave] = best; ri[wave] = bi; }
+    __syncthreads();
+    if (tid == 0) {
+      float bv = rv[0];
+      int bx = ri[0];
+      for (int w = 1; w < NWV; ++w)
+        if (rv[w] > bv || (rv[w] == bv && ri[w] < bx)) { bv = rv[w]; bx = ri[w]; }
+      if (bx >= N) bx = c;  // all entries NaN: keep the diagonal
+      else if (bv == 0.f && info[b] == 0) info[b] = c + 1;
+      ri[NWV] = bx;
+      piv[b * N + c] = bx + 1;
+      pvs[j] = bx;
+    }
+    __syncthreads();
+    const int p = ri[NWV];
+    if (tid < nb) {  // exchange rows c and p on the panel's columns; the pivot row to LDS
+      float* rc = Ab + (size_t)c * N + k0 + tid;
+      float* rp = Ab + (size_t)p * N + k0 + tid;
+      const float vc = *rc, vp = *rp;
+      if (p != c) { *rc = vp; *rp = vc; }
+      prw[tid] = vp;
+    }
+    __syncthreads();
+    const float pv = prw[j];
+    if (pv != 0.f) {
+      const float rcp = 1.0f / pv;
+      for (int r = c + 1 + tid; r < N; r += NT) {
+        float* row = Ab + (size_t)r * N + k0;
+        const float l = row[j] * rcp;
+        row[j] = l;
+        for (int cc = j + 1; cc < nb; ++cc) row[cc] = row[cc] - l * prw[cc];
+      }
+    }
+    __syncthreads();  // the next column's search reads the updated panel; prw is rewritten
   }
+  if (tid < nb) {
+    for (int cc = 0; cc < NB; ++cc) L11[tid][cc] = cc < nb ? Ab[(size_t)(k0 + tid) * N + k0 + cc] : 0.f;
+  }
+  panel_finish<NB>(Ab, N, K0, k0, nb, cend, L11, pvs, prow, pcur, pcnt);
 }
 
 // A[c0.., c0..cend) -= L21 U12 inside the current 64-column block, c0 = k0 + 16: rows
@@ -907,14 +989,16 @@ static int lu_factor_half(int64_t B, int64_t N, int K0, int cend, float* A, int*
         IADMM_CHECK_LAUNCH();
       }
     }
-  } else {  // N > 2048: 8-wide panels on 1024-thread workgroups (N <= kBigMaxM * kBigThreads)
+  } else {  // N > 2048: 8-wide panels on 1024-thread workgroups, in registers while the panel has
+            // <= kBigMaxM * kBigThreads rows, in HBM / L2 above (lu_panel_global_kernel)
     for (int k0 = K0; k0 < cend; k0 += kBigNB) {
       const int R = (int)N - k0;
       const dim3 g((unsigned)B), t(kBigThreads);
       if (R <= 2 * kBigThreads) hipLaunchKernelGGL((lu_panel_kernel<2, kBigNB, kBigThreads>), g, t, 0, s, (int)N, K0, k0, cend, A, piv, info);
       else if (R <= 4 * kBigThreads) hipLaunchKernelGGL((lu_panel_kernel<4, kBigNB, kBigThreads>), g, t, 0, s, (int)N, K0, k0, cend, A, piv, info);
       else if (R <= 8 * kBigThreads) hipLaunchKernelGGL((lu_panel_kernel<8, kBigNB, kBigThreads>), g, t, 0, s, (int)N, K0, k0, cend, A, piv, info);
-      else hipLaunchKernelGGL((lu_panel_kernel<kBigMaxM, kBigNB, kBigThreads>), g, t, 0, s, (int)N, K0, k0, cend, A, piv, info);
+      else if (R <= kBigMaxM * kBigThreads) hipLaunchKernelGGL((lu_panel_kernel<kBigMaxM, kBigNB, kBigThreads>), g, t, 0, s, (int)N, K0, k0, cend, A, piv, info);
+      else hipLaunchKernelGGL((lu_panel_global_kernel<kBigNB, kBigThreads>), g, t, 0, s, (int)N, K0, k0, cend, A, piv, info);
       IADMM_CHECK_LAUNCH();
       const int c0 = k0 + kBigNB;
       if (c0 < cend) {
@@ -1022,7 +1106,7 @@ extern "C" int iadmm_lu_factor(int64_t B, int64_t N, float* A, int* piv, int* in
   if (B <= 0 || N <= 0 || !A || !piv || !info || !ws) return IADMM_E_ARG;
   if (ws_bytes < lu_ws_bytes(B)) return IADMM_E_ARG;
   if (!aligned16(ws)) return IADMM_E_ALIGN;
-  if (N > kBigMaxM * kBigThreads || B > 0x7fffffff) return IADMM_E_SIZE;
+  if (N > kLuMaxN || B > 0x7fffffff) return IADMM_E_SIZE;
   const int64_t ntc_max = (N + kTC - 1) / kTC, nrc_max = (N + kTRW - 1) / kTRW;
   if (B * ntc_max * nrc_max > 0x7fffffff) return IADMM_E_SIZE;
   hipStream_t s = (hipStream_t)stream;

@@ -110,8 +110,9 @@ int iadmm_kkt_rhs(int64_t B, int64_t n, int64_t m, int64_t num_ineq, const float
 /* Stage II batched LU with partial pivoting, in place (replaces torch.lu, models/lu.py:31):
  * A[B,N,N] -> packed L\U; piv[B,N] int32, 1-based like LAPACK getrf / torch.linalg.lu_factor
  * (row i was swapped with row piv[i]-1);
- * info[B] = first 1-based zero pivot or 0.  Right-looking in 64-column blocks (16-column panels up to N = 2048,
- * 8-column panels on 1024-thread workgroups above; MFMA trailing update; limit N <= 10240).
+ * info[B] = first 1-based zero pivot or 0.  Right-looking in 128-column blocks (two 64-column halves; 16-column
+ * panels up to N = 2048, 8-column panels on 1024-thread workgroups above, held in registers up to 10240 panel
+ * rows and in HBM beyond; rank-128 MFMA trailing update; limit N <= 36736, the solve's).
  * ws: caller-owned, 16-B aligned device workspace of at least iadmm_lu_factor_ws_bytes(B, N) bytes
  * (per-instance block permutations); nothing is allocated inside. */
 int64_t iadmm_lu_factor_ws_bytes(int64_t B, int64_t N);

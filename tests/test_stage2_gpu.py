@@ -30,9 +30,10 @@ def _gpu():
 # scalar trailing-update accesses; 1101 also two 1024-row trailing chunks and 4- and 8-slot
 # panels); 400, 2000: several blocks with partial 128-column strips and 64-row steps
 # 2049 .. 10000: the 8-column panels on 1024-thread workgroups (N > 2048; 5003: N % 4 != 0;
-# 10000 = config 4's N, 10 panel rows per thread at the first panel)
+# 10000 = config 4's N, 10 panel rows per thread at the first panel); 12000 / 12291: the first
+# panels exceed the registers' 10240 rows and run from HBM (lu_panel_global_kernel; 12291: N % 4 != 0)
 @pytest.mark.parametrize("N,B", [(16, 2), (37, 3), (64, 2), (100, 2), (130, 2), (257, 2), (400, 2), (1101, 1),
-                                 (2000, 1), (2049, 2), (2500, 1), (5003, 1), (10000, 1)])
+                                 (2000, 1), (2049, 2), (2500, 1), (5003, 1), (10000, 1), (12000, 1), (12291, 1)])
 def test_lu_factor_solve_backward_error(N, B):
     from iadmm import ops
     g = torch.Generator().manual_seed(N)
@@ -77,14 +78,14 @@ def test_lu_pivots_match_lapack_choice(N):
     assert rel_l2(LU, lu_ref) < 1e-5
 
 
-@pytest.mark.parametrize("N", [300, 2000, 2500, 5003])
+@pytest.mark.parametrize("N", [300, 2000, 2500, 5003, 10500])
 def test_lu_recovers_planted_permutation(N):
     """A = P0 L U with well-conditioned unit-lower L and upper U (off-diagonals scaled by
     1/sqrt(N), |diag U| in [1, 2]; cond ~2 and ~5): at every step the row of L's diagonal beats
     every other candidate by > sqrt(N), so partial pivoting must choose exactly P0 (no
     near-ties, unlike random matrices) and the factors must equal L and U to fp32 accuracy (the LU
     of P0^T A is unique; LAPACK sgetrf gives ~1e-7).  Covers both panel shapes (16-wide <= 2048 <
-    8-wide)."""
+    8-wide; 10500: the panels with more than 10240 rows, k0 < 260, from HBM, the rest in registers)."""
     from iadmm import ops
     g = torch.Generator().manual_seed(N)
     s = N ** 0.5
