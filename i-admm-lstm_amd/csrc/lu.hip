@@ -1,23 +1,25 @@
 // Stage II: batched dense LU with partial pivoting and the two triangular solves
 // (reference: models/lu.py:26-35, torch.lu / torch.lu_solve on K[B,N,N]).
 //
-// Right-looking blocked LU in 64-column blocks (the ?getrf structure), each block factored as
-// four 16-column panels (N <= 2048) or eight 8-column panels (2048 < N <= 10240):
+// Right-looking blocked LU (the ?getrf structure) in 128-column outer blocks, each split into two
+// 64-column halves factored as 16-column panels (N <= 2048) or 8-column panels (N > 2048):
 //   lu_panel_kernel        one workgroup per instance: the (N-k) x 16 (x 8) panel is factored in registers
 //                          (pivot = first max |a| like LAPACK i?amax; the multipliers use a
 //                          reciprocal like ?getf2), the row interchanges are applied to the
-//                          block's other columns (?laswp), and U = L11^-1 A is solved for the
-//                          panel rows inside the current 64-column block.
-//   lu_update_block_kernel A -= L21 U12 on the columns of the current block right of the panel
-//                          (<= 48 (56) columns, rows below the panel).
-// and, once per block, on the columns right of it:
-//   lu_swap_trsm_block_kernel the block's row interchanges on the columns outside it, and
-//                          U12 = L11^-1 A12 for its 64 rows (L11 in LDS; one thread per column).
-//   lu_trail_kernel        A22 -= L21 U12, rank 64, on fp32 MFMA (v_mfma_f32_32x32x2f32): 128-column
-//                          strips streamed in 64-row steps, U12^T and -L21 staged in LDS, A22
-//                          loaded into the accumulators and stored back (A22 read + written once
-//                          per 64 columns instead of once per 16: a quarter of the HBM traffic of
-//                          a 16-wide right-looking update).
+//                          half's other columns (?laswp), and U = L11^-1 A is solved for the
+//                          panel rows inside the current half; lu_panel_global_kernel is the
+//                          same column steps with the panel in HBM / L2 (more than 10240 rows).
+//   lu_update_block_kernel A -= L21 U12 on the columns of the current half right of the panel.
+// per 128-column block: first half factored; its interchanges + U12 on the second half
+// (lu_swap_kernel<64, true>); the second half's rank-64 update (lu_trail_kernel, cmax); second
+// half factored; its interchanges on the first half; the block's 128 interchanges composed into
+// one row permutation (lu_block_perm_kernel) applied left and right of the block in one pass
+// (lu_swap_kernel<128, false>); L11^-1 (lu_linv_kernel); then
+//   lu_trail128_kernel     U12 = L11^-1 A12 (MFMA prologue) and A22 -= L21 U12 at rank 128 on fp32
+//                          MFMA (v_mfma_f32_32x32x2f32): 128-column strips streamed in 64-row
+//                          steps, A22 read + written once per 128 columns.
+// IADMM_LU_RANK128=0 selects the r02 flow (64-column blocks, rank-64 lu_trail_kernel, substitution
+// TRSM) for A/B runs.
 // lu_solve_kernel: one workgroup per instance; P b, then blocked forward (unit L) and backward
 // (U) substitution: 64-row blocks, prefix dot products over coalesced row segments, the 64x64
 // diagonal block solved inside one wave.

@@ -114,7 +114,7 @@ int iadmm_kkt_rhs(int64_t B, int64_t n, int64_t m, int64_t num_ineq, const float
  * panels up to N = 2048, 8-column panels on 1024-thread workgroups above, held in registers up to 10240 panel
  * rows and in HBM beyond; rank-128 MFMA trailing update; limit N <= 36736, the solve's).
  * ws: caller-owned, 16-B aligned device workspace of at least iadmm_lu_factor_ws_bytes(B, N) bytes
- * (per-instance block permutations); nothing is allocated inside. */
+ * (per-instance block permutations and the 128x128 L11^-1 blocks); nothing is allocated inside. */
 int64_t iadmm_lu_factor_ws_bytes(int64_t B, int64_t N);
 int iadmm_lu_factor(int64_t B, int64_t N, float* A, int* piv, int* info, void* ws, int64_t ws_bytes,
                     void* stream);
