@@ -4,7 +4,7 @@ The HIP solve (Ruiz -> 100 Stage-I iterations -> unscale) of the bench's first t
 against the CPU oracle on the same instances, for the per-iteration primal/dual residual
 histories and the final iterate.  Two weight sets:
 
-* ``trained`` — checkpoints/QP_1000_500_500_100_800.pth (tools/train_checkpoint.py): the solve
+* ``trained`` — checkpoints/QP_1000_500_500_100_800.pth (the reference recipe, checkpoints/README.md): the solve
   converges, and the stated fp32 contract holds: rel-L2(x^K), rel-L2(z^K) <= 1e-4, primal/dual
   relative error <= 1e-4 at every iteration, y <= 5e-3 (equality-row cancellation).
 * ``random-init`` — the reference's initialisation: the solve diverges at this shape (primal
