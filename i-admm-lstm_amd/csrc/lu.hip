@@ -626,7 +626,12 @@ constexpr int kT2S = 64;          //   rows per pipeline step
 constexpr int kT2K = kOB + 4;     //   LDS stride (k) of the U12^T, -L21 and L11^-1 tiles
 constexpr int kT2CS = kT2C + 8;   //   LDS stride of the A22 staging tile
 constexpr int kT2Threads = 512;
-constexpr size_t kT2Lds = ((size_t)kT2C * kT2K + (size_t)kT2S * kT2K + (size_t)kT2S * kT2CS) * sizeof(float);
+// the block's composed row permutation for the gathered loads: the block rows' sources, the displaced
+// rows below the block with their sources (as given, then sorted) and a bitmap of the displaced rows
+constexpr int kT2BitWords = 2 * ((kLuMaxN + kT2S - 1) / kT2S) + 2;
+constexpr int kT2PermInts = 5 * kPermMax + kT2BitWords;
+constexpr size_t kT2Lds = ((size_t)kT2C * kT2K + (size_t)kT2S * kT2K + (size_t)kT2S * kT2CS) * sizeof(float) +
+                          (size_t)kT2PermInts * sizeof(int);
 static_assert(kT2S * kT2K + kT2S * kT2CS >= kOB * kT2K, "L11^-1 staging must fit in the -L21 + A22 tiles");
 static_assert(kT2Lds <= 160 * 1024, "gfx950 LDS");
 constexpr int kLinvFloats = kOB * kOB;
@@ -666,10 +671,15 @@ __global__ __launch_bounds__(kOB) void lu_linv_kernel(int N, int P, const float*
   for (int i = 0; i < kOB; ++i) out[i * kOB + j] = x[i];
 }
 
-// Fused U12 = L11^-1 A12 and A22 -= L21 U12 (rank 128) for the columns right of [P, P + 128).  One
-// workgroup (8 waves, one per CU) per (instance, 128-column strip), all trailing rows:
-//   prologue: A12 (128 x 128, transposed) and L11^-1 into LDS, U12 on MFMA (each wave two 32 x 32
-//             tiles), written to the block rows of A (final U) and, transposed, into Ut;
+// Fused row interchanges, U12 = L11^-1 A12 and A22 -= L21 U12 (rank 128) for the columns right of
+// [P, P + 128).  One workgroup (8 waves, one per CU) per (instance, 128-column strip), all trailing
+// rows.  The block's 128 interchanges (composed by lu_block_perm_kernel: block row P + i takes row
+// pcur[i], each displaced row below the block takes an original block row) get no pass of their
+// own over these columns: the loads gather through the permutation, and the block rows -- the only
+// sources of displaced rows -- are overwritten (with U12) after the last step's loads.
+// (perm == nullptr: no interchanges, tools/lubench128.hip.)
+//   prologue: the gathered A12 (128 x 128, transposed) and L11^-1 into LDS, U12 on MFMA (each wave
+//             two 32 x 32 tiles), kept in registers for the block rows and, transposed, in Ut;
 //   main loop: 64-row steps, A22 through the LDS staging tile (row-contiguous 16-B global accesses),
 //             -L21 through LDS, next step's A22 / L21 loads in flight during the MFMAs; wave
 //             (wr, wc) owns 32 x 32 of a step (v_mfma_f32_32x32x2f32, 64 per step: lane half h covers
@@ -678,12 +688,18 @@ __global__ __launch_bounds__(kOB) void lu_linv_kernel(int N, int P, const float*
 // DIAG (tools/lubench128.hip only): 1 = no MFMAs in the main loop, 2 = no global A22 / L21 traffic in it.
 template <bool VEC, int DIAG = 0>
 __global__ __launch_bounds__(kT2Threads, 1) void lu_trail128_kernel(int N, int P, int ntc, float* A,
-                                                                    const float* Linv) {
+                                                                    const float* Linv, const int* perm) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   float* Ut = sm;                       // [kT2C cols][kT2K]: U12^T (A12^T in the prologue)
   float* Ls = Ut + kT2C * kT2K;         // [kT2S rows][kT2K]: -L21 of the step
   float* Cb = Ls + kT2S * kT2K;         // [kT2S rows][kT2CS]: A22 rows in, results out
   float* Li = Ls;                       // prologue: L11^-1 [128 rows][kT2K] over Ls + Cb
+  int* bsrc = reinterpret_cast<int*>(Cb + kT2S * kT2CS);  // [128] source row of block row P + i
+  int* tdst = bsrc + kPermMax;          // [128] displaced rows and
+  int* tsrc = tdst + kPermMax;          // [128] their sources, as given;
+  int* ddst = tsrc + kPermMax;          // [128] the same sorted by row
+  int* dsrc = ddst + kPermMax;          // [128]
+  unsigned* dbits = reinterpret_cast<unsigned*>(dsrc + kPermMax);  // 2 words per step: displaced rows
   const int nwg = gridDim.x, bid = blockIdx.x;
   const int xcd = bid & 7, local = bid >> 3, q8 = nwg >> 3, r8 = nwg & 7;
   const int logical = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + local;
@@ -701,6 +717,15 @@ __global__ __launch_bounds__(kT2Threads, 1) void lu_trail128_kernel(int N, int P
   constexpr int kLQ = kT2S * kOB / W / NT;    // -L21 accesses per thread per step
   constexpr int kPQ = kOB * kT2C / W / NT;    // A12 / L11^-1 accesses per thread (prologue)
   constexpr int CPR = kT2C / W, LPR = kOB / W;
+  // main-loop loads: unconditional, from a clamped (valid) address.  Rows >= N / columns >= N only
+  // feed products that are never stored, so they need no zero fill -- and a load with no select
+  // stays out of a branch, which keeps the compiler's vmcnt waits exact (a conditional load costs a
+  // full vmcnt(0) drain at every later use).
+  auto ldu = [&](int row, int col) -> VT {
+    const float* p = Ab + (size_t)row * N + col;
+    if constexpr (VEC) return *reinterpret_cast<const float4*>(p);
+    else return *p;
+  };
   auto ld = [&](int row, int col, bool ok) -> VT {
     const float* p = Ab + (size_t)row * N + col;
     if constexpr (VEC) {
@@ -716,11 +741,39 @@ __global__ __launch_bounds__(kT2Threads, 1) void lu_trail128_kernel(int N, int P
     else *d = sgn * v;
   };
 
+  // ---- the permutation (displaced rows are >= c0 and distinct; <= 128 of them)
+  const int ndisp = perm ? perm[b * kPermInts + 4 * kPermMax] - kOB : 0;
+  {
+    const int* pb = perm + b * kPermInts;
+    if (tid < kOB) bsrc[tid] = perm ? pb[2 * kPermMax + tid] : P + tid;
+    if (tid < ndisp) { tdst[tid] = pb[kOB + tid]; tsrc[tid] = pb[2 * kPermMax + kOB + tid]; }
+    for (int w = tid; w < 2 * nsteps + 2; w += NT) dbits[w] = 0u;  // (+ the one-past-the-end step)
+  }
+  __syncthreads();
+  if (tid < ndisp) {
+    const int d = tdst[tid];
+    int rank = 0;
+    for (int j = 0; j < ndisp; ++j) rank += tdst[j] < d;
+    ddst[rank] = d;
+    dsrc[rank] = tsrc[tid];
+    atomicOr(&dbits[(d - c0) >> 5], 1u << ((d - c0) & 31));
+  }
+  // (published by the barrier after the prologue's LDS fills below)
+  // source row of trailing row `row` (in step `step`; m = that step's bitmap)
+  auto src_row = [&](int row, int ro, unsigned long long m) -> int {
+    if (!((m >> ro) & 1ull)) return row;
+    int lo = 0, hi = ndisp - 1;
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      if (ddst[mid] < row) lo = mid + 1; else hi = mid;
+    }
+    return dsrc[lo];
+  };
   // ---- prologue: U12 = L11^-1 A12 on this strip
 #pragma unroll
   for (int q = 0; q < kPQ; ++q) {  // A12 -> Ut (transposed)
     const int e = tid + NT * q, k = e / CPR, cl = (e % CPR) * W, col = cb + cl;
-    const VT u = ld(P + k, min(col, N - W), col < N);
+    const VT u = ld(bsrc[k], min(col, N - W), col < N);
     if constexpr (VEC) {
       Ut[(cl + 0) * kT2K + k] = u.x; Ut[(cl + 1) * kT2K + k] = u.y;
       Ut[(cl + 2) * kT2K + k] = u.z; Ut[(cl + 3) * kT2K + k] = u.w;
@@ -735,9 +788,9 @@ __global__ __launch_bounds__(kT2Threads, 1) void lu_trail128_kernel(int N, int P
     *reinterpret_cast<float4*>(Li + i * kT2K + kk) = *reinterpret_cast<const float4*>(Lb + (size_t)i * kOB + kk);
   }
   __syncthreads();
+  const int ti = wave >> 1, tj0 = 2 * (wave & 1);
+  floatx16 u0, u1;  // this wave's two U12 tiles: stored to the block rows after the main loop
   {
-    const int ti = wave >> 1, tj0 = 2 * (wave & 1);
-    floatx16 u0, u1;
 #pragma unroll
     for (int v = 0; v < 16; ++v) { u0[v] = 0.f; u1[v] = 0.f; }
 #pragma unroll 4
@@ -759,8 +812,6 @@ __global__ __launch_bounds__(kT2Threads, 1) void lu_trail128_kernel(int N, int P
       const int j0 = tj0 * 32 + il, j1 = j0 + 32;
       Ut[j0 * kT2K + i] = u0[v];
       Ut[j1 * kT2K + i] = u1[v];
-      if (cb + j0 < N) Ab[(size_t)(P + i) * N + cb + j0] = u0[v];
-      if (cb + j1 < N) Ab[(size_t)(P + i) * N + cb + j1] = u1[v];
     }
   }
 
@@ -770,17 +821,18 @@ __global__ __launch_bounds__(kT2Threads, 1) void lu_trail128_kernel(int N, int P
   // step, the next step's A22 / L21 loads in flight during the MFMAs.
   const int wr = (wave >> 2) * 32, wc = (wave & 3) * 32;
   auto loadC = [&](int step, VT (&c)[kCQ]) {
+    const unsigned long long m = *reinterpret_cast<const unsigned long long*>(dbits + 2 * step);
 #pragma unroll
     for (int q = 0; q < kCQ; ++q) {
-      const int e = tid + NT * q, row = c0 + step * kT2S + e / CPR, col = cb + (e % CPR) * W;
-      c[q] = ld(min(row, N - 1), min(col, N - W), row < N && col < N);
+      const int e = tid + NT * q, ro = e / CPR, row = c0 + step * kT2S + ro, col = cb + (e % CPR) * W;
+      c[q] = ldu(min(src_row(row, ro, m), N - 1), min(col, N - W));
     }
   };
   auto loadL = [&](int step, VT (&l)[kLQ]) {
 #pragma unroll
     for (int q = 0; q < kLQ; ++q) {
       const int e = tid + NT * q, row = c0 + step * kT2S + e / LPR;
-      l[q] = ld(min(row, N - 1), P + (e % LPR) * W, row < N);
+      l[q] = ldu(min(row, N - 1), P + (e % LPR) * W);
     }
   };
   auto writeL = [&](const VT (&l)[kLQ]) {
@@ -812,9 +864,9 @@ __global__ __launch_bounds__(kT2Threads, 1) void lu_trail128_kernel(int N, int P
   // LDS in the middle of step s + 1, a step and a half after its loads were issued.
   auto body = [&](int step, VT (&cc)[kCQ], VT (&cn)[kCQ], const VT (&lw)[kLQ], VT (&lnext)[kLQ]) {
     const bool more = step + 1 < nsteps;
-    if (more && DIAG != 2) {
+    if (DIAG != 2) {  // (past the last step: clamped rows, never used)
       loadC(step + 1, cn);
-      if (step + 2 < nsteps) loadL(step + 2, lnext);
+      loadL(step + 2, lnext);
     }
     floatx16 acc;
 #pragma unroll
@@ -845,6 +897,14 @@ __global__ __launch_bounds__(kT2Threads, 1) void lu_trail128_kernel(int N, int P
   for (int step = 0; step < nsteps; step += 2) {
     body(step, c0r, c1r, lb, la);
     if (step + 1 < nsteps) body(step + 1, c1r, c0r, la, lb);
+  }
+  __syncthreads();  // every gathered load of a block row has completed
+#pragma unroll
+  for (int v = 0; v < 16; ++v) {
+    const int i = ti * 32 + 8 * (v >> 2) + 4 * h + (v & 3);
+    const int j0 = tj0 * 32 + il, j1 = j0 + 32;
+    if (cb + j0 < N) Ab[(size_t)(P + i) * N + cb + j0] = u0[v];
+    if (cb + j1 < N) Ab[(size_t)(P + i) * N + cb + j1] = u1[v];
   }
 }
 
@@ -1015,14 +1075,17 @@ static int lu_factor_half(int64_t B, int64_t N, int K0, int cend, float* A, int*
 
 // The interchanges of rows [K0, cend) (cend - K0 <= 128) on the columns [a0, a1) and [b0, b1), with
 // U12 = L11^-1 A12 for the columns [b0, trsm_end) (a 64-row half only).
+// (build = false: perm already holds this block's permutation.)
 static int lu_swap(int64_t B, int64_t N, int K0, int cend, int a0, int a1, int b0, int b1, int trsm_end, float* A,
-                   const int* piv, int* perm, hipStream_t s) {
+                   const int* piv, int* perm, hipStream_t s, bool build = true) {
   a1 = std::max(a0, a1);
   b1 = std::max(b0, b1);
   const int cols = (a1 - a0) + (b1 - b0), nbk = cend - K0;
   if (cols <= 0 || nbk <= 0) return 0;
-  hipLaunchKernelGGL(lu_block_perm_kernel, dim3((unsigned)B), dim3(64), 0, s, (int)N, K0, cend, piv, perm);
-  IADMM_CHECK_LAUNCH();
+  if (build) {
+    hipLaunchKernelGGL(lu_block_perm_kernel, dim3((unsigned)B), dim3(64), 0, s, (int)N, K0, cend, piv, perm);
+    IADMM_CHECK_LAUNCH();
+  }
   const dim3 grid((unsigned)B, (unsigned)((cols + 255) / 256));
   if (trsm_end > b0)
     hipLaunchKernelGGL((lu_swap_kernel<kBlk, true>), grid, dim3(256), 0, s, (int)N, K0, nbk, a0, a1, b0, b1, trsm_end, A, perm);
@@ -1078,16 +1141,20 @@ static int lu_factor_blocks(int64_t B, int64_t N, float* A, int* piv, int* info,
     // second half: factor; its interchanges on the first half's columns
     if (!rc && c1 < n_) rc = lu_factor_half(B, N, c1, c2, A, piv, info, s);
     if (!rc && c1 < n_) rc = lu_swap(B, N, c1, c2, P, c1, 0, 0, 0, A, piv, perm, s);
-    // the whole block's interchanges (composed) on the columns left and right of it, in one pass
-    if (!rc) rc = lu_swap(B, N, P, c2, 0, P, c2, n_, 0, A, piv, perm, s);
+    // the whole block's interchanges composed into one row permutation: applied here to the columns
+    // left of the block, and inside lu_trail128_kernel (gathered loads) to the columns right of it
+    if (rc) break;
+    hipLaunchKernelGGL(lu_block_perm_kernel, dim3((unsigned)B), dim3(64), 0, s, (int)N, P, c2, piv, perm);
+    IADMM_CHECK_LAUNCH();
+    rc = lu_swap(B, N, P, c2, 0, P, 0, 0, 0, A, piv, perm, s, false);
     if (rc || c2 >= n_) break;
     // U12 = L11^-1 A12 and the rank-128 update of everything right of the block
     hipLaunchKernelGGL(lu_linv_kernel, dim3((unsigned)B), dim3(kOB), 0, s, (int)N, P, A, linv);
     IADMM_CHECK_LAUNCH();
     const int ntc = ((int)N - c2 + kT2C - 1) / kT2C;
     const dim3 grid((unsigned)(B * ntc));
-    if (vec) hipLaunchKernelGGL(lu_trail128_kernel<true>, grid, dim3(kT2Threads), kT2Lds, s, (int)N, P, ntc, A, linv);
-    else hipLaunchKernelGGL(lu_trail128_kernel<false>, grid, dim3(kT2Threads), kT2Lds, s, (int)N, P, ntc, A, linv);
+    if (vec) hipLaunchKernelGGL(lu_trail128_kernel<true>, grid, dim3(kT2Threads), kT2Lds, s, (int)N, P, ntc, A, linv, perm);
+    else hipLaunchKernelGGL(lu_trail128_kernel<false>, grid, dim3(kT2Threads), kT2Lds, s, (int)N, P, ntc, A, linv, perm);
     IADMM_CHECK_LAUNCH();
   }
   return rc;
