@@ -113,7 +113,7 @@ IADMM_DEV void panel_finish(float* Ab, int N, int K0, int k0, int nb, int cend, 
     if (col < cend && (col < k0 || col >= k0 + nb)) {
       float v[2 * NB];
 #pragma unroll
-      for (int i = 0; i < 2 * NB; ++i) v[i] = i < cnt ? Ab[(size_t)pcur[i] * N + col] : 0.f;
+      for (int i = 0; i < 2 * NB; ++i) v[i] = Ab[(size_t)pcur[min(i, cnt - 1)] * N + col];  // (unconditional loads)
 #pragma unroll
       for (int i = 0; i < 2 * NB; ++i)
         if (i < cnt) Ab[(size_t)prow[i] * N + col] = v[i];
@@ -124,7 +124,7 @@ IADMM_DEV void panel_finish(float* Ab, int N, int K0, int k0, int nb, int cend, 
   if (c < cend) {
     float x[NB];
 #pragma unroll
-    for (int i = 0; i < NB; ++i) x[i] = i < nb ? Ab[(size_t)(k0 + i) * N + c] : 0.f;
+    for (int i = 0; i < NB; ++i) x[i] = Ab[(size_t)(k0 + min(i, nb - 1)) * N + c];
 #pragma unroll
     for (int i = 1; i < NB; ++i) {
       float s = x[i];
@@ -172,12 +172,10 @@ __global__ __launch_bounds__(NT, NT <= 256 ? 2 : 1) void lu_panel_kernel(int N, 
       }
     } else {
 #pragma unroll
-      for (int c = 0; c < kNB; ++c) a[m][c] = c < nb ? src[c] : 0.f;
+      for (int c = 0; c < kNB; ++c) a[m][c] = src[min(c, nb - 1)];
     }
-    if (r >= R) {
-#pragma unroll
-      for (int c = 0; c < kNB; ++c) a[m][c] = 0.f;
-    }
+    // (no zero fill of rows >= R / columns >= nb: every use below is masked, and overwriting a
+    // register a load is still filling would stall on that load right here)
   }
 
 #pragma unroll
@@ -351,38 +349,61 @@ __global__ __launch_bounds__(NT, 1) void lu_panel_global_kernel(int N, int K0, i
   panel_finish<NB>(Ab, N, K0, k0, nb, cend, L11, pvs, prow, pcur, pcnt);
 }
 
-// A[c0.., c0..cend) -= L21 U12 inside the current 64-column block, c0 = k0 + 16: rows
-// [c0 + blockIdx.y*64, +64) of instance blockIdx.x, w = cend - c0 <= 64 - NB columns.
+// A[c0.., c0..cend) -= L21 U12 inside the current 64-column half, c0 = k0 + NB: rows
+// [c0 + blockIdx.y*64, +64) of instance blockIdx.x, w = cend - c0 <= 64 - NB columns.  Every thread
+// issues all of its loads (U12 and L21 pieces, then its A elements) at once from clamped, valid
+// addresses before it uses any: a fixed count per thread, no loop-carried load -> use -> load chain.
 template <int NB>
 __global__ __launch_bounds__(256) void lu_update_block_kernel(int N, int k0, int cend, float* A) {
-  constexpr int kNB = NB;
-  __shared__ float Us[kNB][kBlk - kNB];
-  __shared__ float Ls[kUpdRows][kNB + 1];
+  constexpr int kW = kBlk - NB;                       // widest update
+  constexpr int kUq = (NB * kW + 255) / 256;          // U12 elements per thread
+  constexpr int kLq = (kUpdRows * NB + 255) / 256;    // L21 elements per thread
+  constexpr int kAq = (kUpdRows * kW + 255) / 256;    // A elements per thread
+  __shared__ float Us[NB][kW];
+  __shared__ float Ls[kUpdRows][NB + 1];
   const int tid = threadIdx.x;
   const size_t b = blockIdx.x;
   float* Ab = A + b * (size_t)N * N;
-  const int c0 = k0 + kNB, w = cend - c0;
+  const int c0 = k0 + NB, w = cend - c0;
   const int r0 = c0 + blockIdx.y * kUpdRows;
   const int rows = min(kUpdRows, N - r0);
   if (rows <= 0 || w <= 0) return;
-  for (int idx = tid; idx < kNB * w; idx += blockDim.x) {
-    const int l = idx / w, c = idx % w;
-    Us[l][c] = Ab[(size_t)(k0 + l) * N + c0 + c];
+  float u[kUq], l[kLq], a[kAq];
+#pragma unroll
+  for (int q = 0; q < kUq; ++q) {
+    const int idx = min(tid + 256 * q, NB * kW - 1), li = idx / kW, c = min(idx % kW, w - 1);
+    u[q] = Ab[(size_t)(k0 + li) * N + c0 + c];
   }
-  for (int idx = tid; idx < rows * kNB; idx += blockDim.x) {
-    const int r = idx / kNB, l = idx % kNB;
-    Ls[r][l] = Ab[(size_t)(r0 + r) * N + k0 + l];
+#pragma unroll
+  for (int q = 0; q < kLq; ++q) {
+    const int idx = min(tid + 256 * q, kUpdRows * NB - 1), r = min(idx / NB, rows - 1), li = idx % NB;
+    l[q] = Ab[(size_t)(r0 + r) * N + k0 + li];
+  }
+#pragma unroll
+  for (int q = 0; q < kAq; ++q) {
+    const int idx = min(tid + 256 * q, kUpdRows * kW - 1), r = min(idx / kW, rows - 1), c = min(idx % kW, w - 1);
+    a[q] = Ab[(size_t)(r0 + r) * N + c0 + c];
+  }
+#pragma unroll
+  for (int q = 0; q < kUq; ++q) {
+    const int idx = tid + 256 * q;
+    if (idx < NB * kW) Us[idx / kW][idx % kW] = u[q];
+  }
+#pragma unroll
+  for (int q = 0; q < kLq; ++q) {
+    const int idx = tid + 256 * q;
+    if (idx < kUpdRows * NB) Ls[idx / NB][idx % NB] = l[q];
   }
   __syncthreads();
-  const int tot = rows * w;
-#pragma unroll 4
-  for (int idx = tid; idx < tot; idx += blockDim.x) {
-    const int r = idx / w, c = idx % w;
-    float* ap = Ab + (size_t)(r0 + r) * N + c0 + c;
-    float a = *ap;
 #pragma unroll
-    for (int l = 0; l < kNB; ++l) a = a - Ls[r][l] * Us[l][c];
-    *ap = a;
+  for (int q = 0; q < kAq; ++q) {
+    const int idx = tid + 256 * q, r = idx / kW, c = idx % kW;
+    if (idx < kUpdRows * kW && r < rows && c < w) {
+      float v = a[q];
+#pragma unroll
+      for (int li = 0; li < NB; ++li) v = v - Ls[r][li] * Us[li][c];
+      Ab[(size_t)(r0 + r) * N + c0 + c] = v;
+    }
   }
 }
 
@@ -432,13 +453,15 @@ __global__ __launch_bounds__(256) void lu_swap_kernel(int N, int K0, int nbk, in
   const int q = blockIdx.y * blockDim.x + tid, na = a1 - a0;
   const int c = q < na ? a0 + q : b0 + (q - na);
   if (q >= na && c >= b1) return;
+  // (all loads unconditional, from valid rows: a conditional load makes the compiler drain every
+  // outstanding load at its use, serialising the column's moves)
   float x[NBK];
 #pragma unroll
-  for (int i = 0; i < NBK; ++i) x[i] = i < nbk ? Ab[(size_t)pcur[i] * N + c] : 0.f;
+  for (int i = 0; i < NBK; ++i) x[i] = Ab[(size_t)pcur[min(i, nbk - 1)] * N + c];
   for (int i0 = nbk; i0 < cnt; i0 += 16) {
     float y[16];
 #pragma unroll
-    for (int i = 0; i < 16; ++i) y[i] = i0 + i < cnt ? Ab[(size_t)pcur[i0 + i] * N + c] : 0.f;
+    for (int i = 0; i < 16; ++i) y[i] = Ab[(size_t)pcur[min(i0 + i, cnt - 1)] * N + c];
 #pragma unroll
     for (int i = 0; i < 16; ++i)
       if (i0 + i < cnt) Ab[(size_t)prow[i0 + i] * N + c] = y[i];
@@ -630,9 +653,11 @@ constexpr int kT2Threads = 512;
 // rows below the block with their sources (as given, then sorted) and a bitmap of the displaced rows
 constexpr int kT2BitWords = 2 * ((kLuMaxN + kT2S - 1) / kT2S) + 2;
 constexpr int kT2PermInts = 5 * kPermMax + kT2BitWords;
-constexpr size_t kT2Lds = ((size_t)kT2C * kT2K + (size_t)kT2S * kT2K + (size_t)kT2S * kT2CS) * sizeof(float) +
+// -L21 and the product tile double-buffered; the prologue's U12^T over the former, L11^-1 over the latter
+constexpr size_t kT2Lds = (2 * (size_t)kT2S * kT2K + 2 * (size_t)kT2S * kT2CS) * sizeof(float) +
                           (size_t)kT2PermInts * sizeof(int);
-static_assert(kT2S * kT2K + kT2S * kT2CS >= kOB * kT2K, "L11^-1 staging must fit in the -L21 + A22 tiles");
+static_assert(2 * kT2S * kT2K >= kT2C * kT2K, "U12^T staging must fit in the -L21 tiles");
+static_assert(2 * kT2S * kT2CS >= kOB * kT2K, "L11^-1 staging must fit in the product tiles");
 static_assert(kT2Lds <= 160 * 1024, "gfx950 LDS");
 constexpr int kLinvFloats = kOB * kOB;
 
@@ -679,22 +704,27 @@ __global__ __launch_bounds__(kOB) void lu_linv_kernel(int N, int P, const float*
 // sources of displaced rows -- are overwritten (with U12) after the last step's loads.
 // (perm == nullptr: no interchanges, tools/lubench128.hip.)
 //   prologue: the gathered A12 (128 x 128, transposed) and L11^-1 into LDS, U12 on MFMA (each wave
-//             two 32 x 32 tiles), kept in registers for the block rows and, transposed, in Ut;
-//   main loop: 64-row steps, A22 through the LDS staging tile (row-contiguous 16-B global accesses),
-//             -L21 through LDS, next step's A22 / L21 loads in flight during the MFMAs; wave
-//             (wr, wc) owns 32 x 32 of a step (v_mfma_f32_32x32x2f32, 64 per step: lane half h covers
-//             k in [64h, 64h + 64)).
+//             two 32 x 32 tiles), transposed into LDS, then each wave's MFMA operand of it -- column
+//             wc + il, k in [64h, 64h + 64): 64 registers -- kept in registers for the whole loop;
+//   main loop: 64-row steps; wave (wr, wc) owns 32 x 32 of a step (v_mfma_f32_32x32x2f32, 64 per
+//             step, -L21 from LDS, U12 from registers).  -L21 and the product tile are
+//             double-buffered in LDS, so a step needs ONE barrier: per wave, step t = issue the
+//             loads of A22 (t + 1) and L21 (t + 2); the MFMAs; product -> Cb[t & 1]; L21 (t + 1)
+//             -> Ls[(t + 1) & 1]; barrier; out = A22 - product for step t (row-contiguous 16-B
+//             global stores, the A22 values already in the registers of the storing thread).  Waves
+//             leave the barrier together but no longer wait for each other's output phase, which
+//             runs beside other waves' MFMAs.
 // Strips of one instance are consecutive logical ids on one XCD (its L2 serves the L21 re-reads).
 // DIAG (tools/lubench128.hip only): 1 = no MFMAs in the main loop, 2 = no global A22 / L21 traffic in it.
 template <bool VEC, int DIAG = 0>
 __global__ __launch_bounds__(kT2Threads, 1) void lu_trail128_kernel(int N, int P, int ntc, float* A,
                                                                     const float* Linv, const int* perm) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
-  float* Ut = sm;                       // [kT2C cols][kT2K]: U12^T (A12^T in the prologue)
-  float* Ls = Ut + kT2C * kT2K;         // [kT2S rows][kT2K]: -L21 of the step
-  float* Cb = Ls + kT2S * kT2K;         // [kT2S rows][kT2CS]: A22 rows in, results out
-  float* Li = Ls;                       // prologue: L11^-1 [128 rows][kT2K] over Ls + Cb
-  int* bsrc = reinterpret_cast<int*>(Cb + kT2S * kT2CS);  // [128] source row of block row P + i
+  float* Ls0 = sm;                      // 2 x [kT2S rows][kT2K]: -L21 of a step
+  float* Cb0 = sm + 2 * kT2S * kT2K;    // 2 x [kT2S rows][kT2CS]: product of a step
+  float* Ut = Ls0;                      // prologue: A12^T, then U12^T [kT2C cols][kT2K], over Ls
+  float* Li = Cb0;                      // prologue: L11^-1 [128 rows][kT2K], over Cb
+  int* bsrc = reinterpret_cast<int*>(Cb0 + 2 * kT2S * kT2CS);  // [128] source row of block row P + i
   int* tdst = bsrc + kPermMax;          // [128] displaced rows and
   int* tsrc = tdst + kPermMax;          // [128] their sources, as given;
   int* ddst = tsrc + kPermMax;          // [128] the same sorted by row
@@ -736,9 +766,9 @@ __global__ __launch_bounds__(kT2Threads, 1) void lu_trail128_kernel(int N, int P
       return ok ? x : 0.f;
     }
   };
-  auto st_lds = [&](float* d, const VT& v, float sgn) {
-    if constexpr (VEC) *reinterpret_cast<float4*>(d) = make_float4(sgn * v.x, sgn * v.y, sgn * v.z, sgn * v.w);
-    else *d = sgn * v;
+  auto st_lds = [&](float* d, const VT& v) {
+    if constexpr (VEC) *reinterpret_cast<float4*>(d) = v;
+    else *d = v;
   };
 
   // ---- the permutation (displaced rows are >= c0 and distinct; <= 128 of them)
@@ -759,7 +789,7 @@ __global__ __launch_bounds__(kT2Threads, 1) void lu_trail128_kernel(int N, int P
     atomicOr(&dbits[(d - c0) >> 5], 1u << ((d - c0) & 31));
   }
   // (published by the barrier after the prologue's LDS fills below)
-  // source row of trailing row `row` (in step `step`; m = that step's bitmap)
+  // source row of trailing row `row` (ro = row - the step's first row; m = that step's bitmap)
   auto src_row = [&](int row, int ro, unsigned long long m) -> int {
     if (!((m >> ro) & 1ull)) return row;
     int lo = 0, hi = ndisp - 1;
@@ -769,6 +799,7 @@ __global__ __launch_bounds__(kT2Threads, 1) void lu_trail128_kernel(int N, int P
     }
     return dsrc[lo];
   };
+
   // ---- prologue: U12 = L11^-1 A12 on this strip
 #pragma unroll
   for (int q = 0; q < kPQ; ++q) {  // A12 -> Ut (transposed)
@@ -788,9 +819,9 @@ __global__ __launch_bounds__(kT2Threads, 1) void lu_trail128_kernel(int N, int P
     *reinterpret_cast<float4*>(Li + i * kT2K + kk) = *reinterpret_cast<const float4*>(Lb + (size_t)i * kOB + kk);
   }
   __syncthreads();
-  const int ti = wave >> 1, tj0 = 2 * (wave & 1);
-  floatx16 u0, u1;  // this wave's two U12 tiles: stored to the block rows after the main loop
   {
+    const int ti = wave >> 1, tj0 = 2 * (wave & 1);
+    floatx16 u0, u1;
 #pragma unroll
     for (int v = 0; v < 16; ++v) { u0[v] = 0.f; u1[v] = 0.f; }
 #pragma unroll 4
@@ -809,17 +840,19 @@ __global__ __launch_bounds__(kT2Threads, 1) void lu_trail128_kernel(int N, int P
 #pragma unroll
     for (int v = 0; v < 16; ++v) {
       const int i = ti * 32 + 8 * (v >> 2) + 4 * h + (v & 3);
-      const int j0 = tj0 * 32 + il, j1 = j0 + 32;
-      Ut[j0 * kT2K + i] = u0[v];
-      Ut[j1 * kT2K + i] = u1[v];
+      Ut[(tj0 * 32 + il) * kT2K + i] = u0[v];
+      Ut[(tj0 * 32 + 32 + il) * kT2K + i] = u1[v];
     }
   }
-
-  // ---- main loop: A22 -= L21 U12.  Per step: the product L21 U12 from zero on MFMA, then
-  // out = A22 - product where the A22 values are already in registers (each thread stores exactly
-  // the elements it prefetched), so A22 never passes through LDS on the way in: two barriers per
-  // step, the next step's A22 / L21 loads in flight during the MFMAs.
+  __syncthreads();
   const int wr = (wave >> 2) * 32, wc = (wave & 3) * 32;
+  float4 ub[kOB / 8];  // U12[64h + 4sg + 0..3][wc + il]: this wave's MFMA operand for every step
+#pragma unroll
+  for (int sg = 0; sg < kOB / 8; ++sg)
+    ub[sg] = *reinterpret_cast<const float4*>(Ut + (wc + il) * kT2K + (kOB / 2) * h + 4 * sg);
+  __syncthreads();  // Ut consumed: Ls from here on
+
+  // ---- main loop
   auto loadC = [&](int step, VT (&c)[kCQ]) {
     const unsigned long long m = *reinterpret_cast<const unsigned long long*>(dbits + 2 * step);
 #pragma unroll
@@ -835,35 +868,37 @@ __global__ __launch_bounds__(kT2Threads, 1) void lu_trail128_kernel(int N, int P
       l[q] = ldu(min(row, N - 1), P + (e % LPR) * W);
     }
   };
-  auto writeL = [&](const VT (&l)[kLQ]) {
+  auto writeL = [&](float* Ls, const VT (&l)[kLQ]) {
 #pragma unroll
     for (int q = 0; q < kLQ; ++q) {
       const int e = tid + NT * q;
-      st_lds(Ls + (e / LPR) * kT2K + (e % LPR) * W, l[q], 1.f);
+      st_lds(Ls + (e / LPR) * kT2K + (e % LPR) * W, l[q]);
     }
   };
-  auto storeOut = [&](int step, const VT (&c)[kCQ]) {
+  // (the result overwrites c in place and is stored from there: a store's data registers stay busy
+  // until the store completes, and c is not reloaded until the next step but one)
+  auto storeOut = [&](int step, const float* Cb, VT (&c)[kCQ]) {
 #pragma unroll
     for (int q = 0; q < kCQ; ++q) {
       const int e = tid + NT * q, row = c0 + step * kT2S + e / CPR, col = cb + (e % CPR) * W;
+      const float* src = Cb + (e / CPR) * kT2CS + (e % CPR) * W;
+      if constexpr (VEC) {
+        const float4 pr = *reinterpret_cast<const float4*>(src);
+        c[q].x -= pr.x; c[q].y -= pr.y; c[q].z -= pr.z; c[q].w -= pr.w;
+      } else {
+        c[q] -= *src;
+      }
       if (row < N && col < N) {
-        const float* src = Cb + (e / CPR) * kT2CS + (e % CPR) * W;
-        if constexpr (VEC) {
-          const float4 pr = *reinterpret_cast<const float4*>(src);
-          *reinterpret_cast<float4*>(Ab + (size_t)row * N + col) =
-              make_float4(c[q].x - pr.x, c[q].y - pr.y, c[q].z - pr.z, c[q].w - pr.w);
-        } else {
-          Ab[(size_t)row * N + col] = c[q] - *src;
-        }
+        if constexpr (VEC) *reinterpret_cast<float4*>(Ab + (size_t)row * N + col) = c[q];
+        else Ab[(size_t)row * N + col] = c[q];
       }
     }
   };
 
-  // A22 of step s + 1 and L21 of step s + 2 are loaded during step s (two register sets each,
-  // alternating roles: the loop is unrolled by two so no register copy waits on a load): L21 goes to
-  // LDS in the middle of step s + 1, a step and a half after its loads were issued.
+  // step t (cc = A22 (t), loaded during step t - 1; lw = L21 (t + 1), loaded during step t - 1)
   auto body = [&](int step, VT (&cc)[kCQ], VT (&cn)[kCQ], const VT (&lw)[kLQ], VT (&lnext)[kLQ]) {
-    const bool more = step + 1 < nsteps;
+    const float* Ls = Ls0 + (step & 1) * (kT2S * kT2K);
+    float* Cb = Cb0 + (step & 1) * (kT2S * kT2CS);
     if (DIAG != 2) {  // (past the last step: clamped rows, never used)
       loadC(step + 1, cn);
       loadL(step + 2, lnext);
@@ -872,39 +907,81 @@ __global__ __launch_bounds__(kT2Threads, 1) void lu_trail128_kernel(int N, int P
 #pragma unroll
     for (int v = 0; v < 16; ++v) acc[v] = 0.f;
     if constexpr (DIAG != 1) {
-#pragma unroll 4
+#pragma unroll
       for (int sg = 0; sg < kOB / 8; ++sg) {
         const float4 fa = *reinterpret_cast<const float4*>(Ls + (wr + il) * kT2K + (kOB / 2) * h + 4 * sg);
-        const float4 fb = *reinterpret_cast<const float4*>(Ut + (wc + il) * kT2K + (kOB / 2) * h + 4 * sg);
 #pragma unroll
-        for (int s4 = 0; s4 < 4; ++s4) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(get4(fa, s4), get4(fb, s4), acc, 0, 0, 0);
+        for (int s4 = 0; s4 < 4; ++s4) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(get4(fa, s4), get4(ub[sg], s4), acc, 0, 0, 0);
       }
     }
-    __syncthreads();  // Ls consumed by every wave; the previous step's Cb reads are done
 #pragma unroll
     for (int v = 0; v < 16; ++v) Cb[(wr + 8 * (v >> 2) + 4 * h + (v & 3)) * kT2CS + wc + il] = acc[v];
-    if (more) writeL(lw);
-    __syncthreads();  // Cb holds this step's product, Ls the next step's L21
-    if (DIAG != 2) storeOut(step, cc);
+    writeL(Ls0 + ((step + 1) & 1) * (kT2S * kT2K), lw);
+    __syncthreads();  // Cb[t & 1] = product (t), Ls[(t + 1) & 1] = L21 (t + 1); Ls[t & 1] consumed
+    if (DIAG != 2) storeOut(step, Cb, cc);
   };
 
-  VT c0r[kCQ], c1r[kCQ], la[kLQ], lb[kLQ];
-  loadC(0, c0r);
-  loadL(0, la);
-  if (nsteps > 1) loadL(1, lb);
-  writeL(la);  // Ls: the prologue's last reads of Li finished before the barrier above
-  __syncthreads();
-  for (int step = 0; step < nsteps; step += 2) {
-    body(step, c0r, c1r, lb, la);
-    if (step + 1 < nsteps) body(step + 1, c1r, c0r, la, lb);
-  }
-  __syncthreads();  // every gathered load of a block row has completed
+  if constexpr (VEC) {
+    VT c0r[kCQ], c1r[kCQ], la[kLQ], lb[kLQ];
+    loadC(0, c0r);
+    loadL(0, la);
+    loadL(1, lb);
+    writeL(Ls0, la);
+    __syncthreads();
+    // pairs of steps, the odd last one after the loop: no conditional body inside the loop, whose
+    // merge would make the compiler copy the register sets (waiting on their loads to do so)
+    int step = 0;
+    for (; step + 1 < nsteps; step += 2) {
+      body(step, c0r, c1r, lb, la);
+      body(step + 1, c1r, c0r, la, lb);
+    }
+    if (step < nsteps) body(step, c0r, c1r, lb, la);
+  } else {
+    // scalar path (N % 4 != 0: 16 single-float accesses per thread and array): one register set
+    // each, the next step's loads issued after the output (the double sets spill here)
+    VT c[kCQ], l[kLQ];
+    loadC(0, c);
+    loadL(0, l);
+    writeL(Ls0, l);
+    loadL(1, l);
+    __syncthreads();
+    for (int step = 0; step < nsteps; ++step) {
+      const float* Ls = Ls0 + (step & 1) * (kT2S * kT2K);
+      float* Cb = Cb0 + (step & 1) * (kT2S * kT2CS);
+      floatx16 acc;
 #pragma unroll
-  for (int v = 0; v < 16; ++v) {
-    const int i = ti * 32 + 8 * (v >> 2) + 4 * h + (v & 3);
-    const int j0 = tj0 * 32 + il, j1 = j0 + 32;
-    if (cb + j0 < N) Ab[(size_t)(P + i) * N + cb + j0] = u0[v];
-    if (cb + j1 < N) Ab[(size_t)(P + i) * N + cb + j1] = u1[v];
+      for (int v = 0; v < 16; ++v) acc[v] = 0.f;
+      if constexpr (DIAG != 1) {
+#pragma unroll
+        for (int sg = 0; sg < kOB / 8; ++sg) {
+          const float4 fa = *reinterpret_cast<const float4*>(Ls + (wr + il) * kT2K + (kOB / 2) * h + 4 * sg);
+#pragma unroll
+          for (int s4 = 0; s4 < 4; ++s4) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(get4(fa, s4), get4(ub[sg], s4), acc, 0, 0, 0);
+        }
+      }
+#pragma unroll
+      for (int v = 0; v < 16; ++v) Cb[(wr + 8 * (v >> 2) + 4 * h + (v & 3)) * kT2CS + wc + il] = acc[v];
+      writeL(Ls0 + ((step + 1) & 1) * (kT2S * kT2K), l);
+      __syncthreads();
+      if (DIAG != 2) {
+        storeOut(step, Cb, c);
+        loadC(step + 1, c);
+        loadL(step + 2, l);
+      }
+    }
+  }
+  __syncthreads();  // every gathered load of a block row has completed: U12 to the block rows
+  if (cb + wc + il < N) {
+#pragma unroll
+    for (int sg = 0; sg < kOB / 8; ++sg) {  // (static register index: the two waves with the same
+      if ((sg >= kOB / 16) != (wave >= 4)) continue;  //  columns split the rows)
+      const int i = (kOB / 2) * h + 4 * sg;
+      float* dst = Ab + (size_t)(P + i) * N + cb + wc + il;
+      dst[0] = ub[sg].x;
+      dst[(size_t)N] = ub[sg].y;
+      dst[2 * (size_t)N] = ub[sg].z;
+      dst[3 * (size_t)N] = ub[sg].w;
+    }
   }
 }
 
