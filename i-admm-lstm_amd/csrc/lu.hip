@@ -987,9 +987,12 @@ __global__ __launch_bounds__(kT2Threads, 1) void lu_trail128_kernel(int N, int P
 
 // Solve (P^T L U) x = b in place for one instance per workgroup.
 constexpr int kDS = kSolveBlk + 1;  // LDS stride of the staged diagonal block
+#ifndef IADMM_SOLVE_LAZY_PIV
+#define IADMM_SOLVE_LAZY_PIV 1
+#endif
 // VEC (N % 4 == 0, 16-B aligned factors): block bounds are multiples of 4, rows 16-B aligned.
 template <bool VEC>
-__global__ __launch_bounds__(kSolveThreads) void lu_solve_kernel(int N, const float* LU, const int* piv,
+__global__ __launch_bounds__(kSolveThreads, 4) void lu_solve_kernel(int N, const float* LU, const int* piv,
                                                               float* X) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   float* x = sm;                  // N
@@ -999,24 +1002,53 @@ __global__ __launch_bounds__(kSolveThreads) void lu_solve_kernel(int N, const fl
   const size_t b = blockIdx.x;
   const float* M = LU + b * (size_t)N * N;
   float* xb = X + b * N;
-  for (int i = tid; i < N; i += blockDim.x) x[i] = xb[i];
+#pragma unroll 8
+  for (int i = tid; i < N; i += kSolveThreads) x[i] = xb[i];
   __syncthreads();
-  if (tid == 0) {
-    for (int i = 0; i < N; ++i) {
-      const int p = piv[b * N + i] - 1;
-      if (p != i) { const float t = x[i]; x[i] = x[p]; x[p] = t; }
+  if (!IADMM_SOLVE_LAZY_PIV && wave == 0) {  // all interchanges up front, 64 pivots per load
+    for (int i0 = 0; i0 < N; i0 += 64) {
+      const int pv = piv[b * N + min(i0 + lane, N - 1)] - 1;
+      const int n = min(64, N - i0);
+      for (int j = 0; j < n; ++j) {
+        const int p = __shfl(pv, j, 64);
+        if (lane == 0 && p != i0 + j) { const float t = x[i0 + j]; x[i0 + j] = x[p]; x[p] = t; }
+      }
     }
   }
   __syncthreads();
+  // The row interchanges (P b) are applied lazily, block by block: interchange i touches positions i
+  // and piv[i] - 1 >= i only, so positions below k0 are final once those of rows < k0 are done.  Wave 0
+  // applies a block's 64 (pivots loaded once per block, broadcast by shuffle) while the other waves'
+  // dot products read only x[0, k0).  (r03: one thread looping over all N with a global load per
+  // interchange was a serial chain of N memory latencies at the start of every solve.)
   for (int pass = 0; pass < 2; ++pass) {  // 0: forward with unit L, 1: backward with U
     const int nblk = (N + kSolveBlk - 1) / kSolveBlk;
     for (int bb = 0; bb < nblk; ++bb) {
       const int k0 = pass == 0 ? bb * kSolveBlk : max(0, N - (bb + 1) * kSolveBlk);
       const int k1 = pass == 0 ? min(N, k0 + kSolveBlk) : N - bb * kSolveBlk;
       const int nbk = k1 - k0;
-      for (int idx = tid; idx < nbk * nbk; idx += blockDim.x) {
-        const int r = idx / nbk, c = idx % nbk;
-        D[r * kDS + c] = M[(size_t)(k0 + r) * N + k0 + c];
+      // the diagonal block: every thread issues its loads at once (clamped, valid addresses; the
+      // entries past nbk are never read), the LDS writes after the dot products below
+      constexpr int kDQ = kSolveBlk * kSolveBlk / kSolveThreads;
+      {
+        float dreg[kDQ];
+#pragma unroll
+        for (int q = 0; q < kDQ; ++q) {
+          const int idx = tid + kSolveThreads * q, r = min(idx / kSolveBlk, nbk - 1), c = min(idx % kSolveBlk, nbk - 1);
+          dreg[q] = M[(size_t)(k0 + r) * N + k0 + c];
+        }
+#pragma unroll
+        for (int q = 0; q < kDQ; ++q) {
+          const int idx = tid + kSolveThreads * q;
+          D[(idx / kSolveBlk) * kDS + idx % kSolveBlk] = dreg[q];
+        }
+      }
+      if (IADMM_SOLVE_LAZY_PIV && pass == 0 && wave == 0) {
+        const int pv = piv[b * N + k0 + min(lane, nbk - 1)] - 1;
+        for (int j = 0; j < nbk; ++j) {
+          const int p = __shfl(pv, j, 64);
+          if (lane == 0 && p != k0 + j) { const float t = x[k0 + j]; x[k0 + j] = x[p]; x[p] = t; }
+        }
       }
       // prefix (forward) / suffix (backward) dot products of the block rows with x: all rows of a
       // block share the column range, so a wave takes 4 rows at a time (16-B loads, 8 in flight
@@ -1084,7 +1116,8 @@ __global__ __launch_bounds__(kSolveThreads) void lu_solve_kernel(int N, const fl
       __syncthreads();
     }
   }
-  for (int i = tid; i < N; i += blockDim.x) xb[i] = x[i];
+#pragma unroll 8
+  for (int i = tid; i < N; i += kSolveThreads) xb[i] = x[i];
 }
 
 // b~ = [sigma x - p ; z - y / rho]  (models/lu.py:125,129)

@@ -1,7 +1,7 @@
 """A/B of the batched LU factorization (csrc/lu.hip) between library builds, on the GPU box.
 
 For each library (IADMM_LIB_PATH) in a child process: factor a batch of KKT matrices at the given
-shape a few times (hipEvents), and check the backward error of one solve against fp64.  Prints one
+shape a few times and one solve five times (hipEvents), and check the backward error of one solve against fp64.  Prints one
 JSON line per library.
 
   python tools/lu_ab.py --libs i-admm-lstm_amd/iadmm/libiadmm.so variants/lu64.so --batch 1024 --N 2000
@@ -41,6 +41,14 @@ def child(args):
     g = torch.Generator(device="cuda").manual_seed(1)
     b = torch.randn(B, args.N, device="cuda", generator=g)
     x = ops.lu_solve(LU, piv, b)
+    solve_ms = []
+    for _ in range(5):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        ops.lu_solve(LU, piv, b)
+        e1.record()
+        torch.cuda.synchronize()
+        solve_ms.append(e0.elapsed_time(e1))
     K = ops.kkt_assemble(d["Q"][:4], d["A0"][:4], 6e-6, None, 0, rho_rows=rho[:4].contiguous()).double()
     xd, bd = x[:4].double(), b[:4].double()
     res = torch.bmm(K, xd.unsqueeze(-1)).squeeze(-1) - bd
@@ -49,7 +57,8 @@ def child(args):
     ms = min(times)
     print(json.dumps({"lib": os.environ.get("IADMM_LIB_PATH", "default"), "B": B, "N": N, "factor_ms": times,
                       "best_ms": ms, "tflops": B * 2.0 / 3.0 * N ** 3 / ms / 1e9, "frac_fp32_mfma": B * 2.0 / 3.0 * N ** 3 / ms / 1e9 / 157.3,
-                      "info_max": int(info.max()), "backward_error": berr, "piv_head": piv[0, :8].tolist()}), flush=True)
+                      "info_max": int(info.max()), "solve_ms": solve_ms,
+                      "solve_tbps": B * args.N * args.N * 4 / min(solve_ms) / 1e9, "backward_error": berr, "piv_head": piv[0, :8].tolist()}), flush=True)
 
 
 def main():
