@@ -84,10 +84,13 @@ IADMM_DEV void build_row_perm(const int* pv, int base, int n, int* rowid, int* c
 }
 
 // The (N-k0) x 16 panel lives in registers: thread t owns rows t + 256 m (m < M), 16 columns
-// each.  Per column j: argmax |a| (thread scan, wave shuffle tree, 4-wave combine in LDS; first
-// index on ties), the owners of rows j and p exchange them through LDS, every thread scales its
-// rows below j by the reciprocal and applies the rank-1 update in registers.  M = ceil((N-k0)/256)
-// rounded up to the next instantiated size.
+// each.  Per column j: argmax |a| (thread scan, wave shuffle tree; first index on ties); each
+// wave's winner writes its whole row to LDS beside the wave's |a| and index, the owner of row j
+// writes row j; one barrier; every thread then combines the waves' winners itself, the owners of
+// rows j and p take their new rows from LDS, and every thread scales its rows below j by the
+// reciprocal and applies the rank-1 update in registers.  One barrier per column (r02/r03: three,
+// with one thread combining the waves between two of them); the LDS is double-buffered by column
+// parity.  M = ceil((N-k0)/256) rounded up to the next instantiated size.
 template <int NB>
 IADMM_DEV float col_of(const float (&row)[NB], int j) {  // row[j] for a run-time j, registers only
   float v = row[0];
@@ -131,6 +134,9 @@ IADMM_DEV void panel_finish(float* Ab, int N, int K0, int k0, int nb, int cend, 
 #pragma unroll
       for (int l = 0; l < i; ++l) s = s - L11[i][l] * x[l];
       x[i] = s;
+      // (one row's L11 reads at a time: hoisting all 120 of them would cost the panel kernels
+      // their fourth workgroup per CU)
+      __builtin_amdgcn_sched_barrier(0);
     }
 #pragma unroll
     for (int i = 0; i < NB; ++i)
@@ -144,13 +150,16 @@ IADMM_DEV void panel_finish(float* Ab, int N, int K0, int k0, int nb, int cend, 
 // workgroup allows; 12 rows spill), so the pivot search still sees the whole column without
 // leaving registers.
 template <int M, int NB, int NT>
-__global__ __launch_bounds__(NT, NT <= 256 ? 2 : 1) void lu_panel_kernel(int N, int K0, int k0, int cend, float* A,
+__global__ __launch_bounds__(NT, NT <= 256 ? (M <= 6 ? 4 : 2) : 1) void lu_panel_kernel(int N, int K0, int k0, int cend, float* A,
                                                                          int* piv, int* info) {
   constexpr int kNB = NB, kLuThreads = NT, NWV = NT / 64;
-  __shared__ float xrow[2][kNB];            // [0] = row j, [1] = pivot row (after the exchange: row j)
+  // per column, double-buffered (index j & 1) so a column costs one barrier: each wave's
+  // candidate pivot row, its |a| and index, and row j before the exchange
+  __shared__ float cand[2][NWV][kNB];
+  __shared__ float rowj[2][kNB];
   __shared__ float L11[kNB][kNB + 1];
-  __shared__ float rv[NWV];
-  __shared__ int ri[NWV + 1];
+  __shared__ float rv[2][NWV];
+  __shared__ int ri[2][NWV];
   __shared__ int pvs[kNB], prow[2 * kNB], pcur[2 * kNB], pcnt[1];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const size_t b = blockIdx.x;
@@ -181,6 +190,7 @@ __global__ __launch_bounds__(NT, NT <= 256 ? 2 : 1) void lu_panel_kernel(int N, 
 #pragma unroll
   for (int j = 0; j < kNB; ++j) {
     if (j < nb) {
+      const int q = j & 1;
       float best = -1.f;
       int bi = R;
 #pragma unroll
@@ -195,46 +205,53 @@ __global__ __launch_bounds__(NT, NT <= 256 ? 2 : 1) void lu_panel_kernel(int N, 
         const int oi = __shfl_xor(bi, o, 64);
         if (ov > best || (ov == best && oi < bi)) { best = ov; bi = oi; }
       }
-      if (lane == 0) { rv[wave] = best; ri[wave] = bi; }
+      // the wave's winner (a row of one of its own lanes) publishes its whole row, so no second
+      // round trip is needed once the waves' winners are compared
+#pragma unroll
+      for (int m = 0; m < M; ++m)
+        if (tid + kLuThreads * m == bi) {
+#pragma unroll
+          for (int c = 0; c < kNB; ++c) cand[q][wave][c] = a[m][c];
+        }
+      if (lane == 0) { rv[q][wave] = best; ri[q][wave] = bi; }
       if (tid == j) {
 #pragma unroll
-        for (int c = 0; c < kNB; ++c) xrow[0][c] = a[0][c];
+        for (int c = 0; c < kNB; ++c) rowj[q][c] = a[0][c];
       }
       __syncthreads();
+      // every thread combines the waves' winners (same order and tie rule as the shuffle tree)
+      float bv = rv[q][0];
+      int bx = ri[q][0], bw = 0;
+#pragma unroll
+      for (int w = 1; w < NWV; ++w) {
+        const float ov = rv[q][w];
+        const int oi = ri[q][w];
+        if (ov > bv || (ov == bv && oi < bx)) { bv = ov; bx = oi; bw = w; }
+      }
+      const bool nan_col = bx >= R;  // all entries NaN: keep the diagonal
+      const int p = nan_col ? j : bx;
       if (tid == 0) {
-        float bv = rv[0];
-        int bx = ri[0];
-        for (int w = 1; w < NWV; ++w)
-          if (rv[w] > bv || (rv[w] == bv && ri[w] < bx)) { bv = rv[w]; bx = ri[w]; }
-        if (bx >= R) bx = j;  // all entries NaN: keep the diagonal
-        else if (bv == 0.f && info[b] == 0) info[b] = k0 + j + 1;
-        ri[NWV] = bx;
-        piv[b * N + k0 + j] = k0 + bx + 1;
-        pvs[j] = k0 + bx;
+        if (!nan_col && bv == 0.f && info[b] == 0) info[b] = k0 + j + 1;
+        piv[b * N + k0 + j] = k0 + p + 1;
+        pvs[j] = k0 + p;
       }
-      __syncthreads();
-      const int p = ri[NWV];
-      // the owner of row p publishes it and takes row j's values
+      float pr[kNB];
+#pragma unroll
+      for (int c = 0; c < kNB; ++c) pr[c] = nan_col ? rowj[q][c] : cand[q][bw][c];
+      // the owner of row p takes row j's values, the owner of row j the pivot row
 #pragma unroll
       for (int m = 0; m < M; ++m)
         if (tid + kLuThreads * m == p) {
 #pragma unroll
-          for (int c = 0; c < kNB; ++c) {
-            xrow[1][c] = a[m][c];
-            a[m][c] = xrow[0][c];
-          }
+          for (int c = 0; c < kNB; ++c) a[m][c] = rowj[q][c];
         }
-      __syncthreads();
       if (tid == j) {
 #pragma unroll
-        for (int c = 0; c < kNB; ++c) a[0][c] = xrow[1][c];
+        for (int c = 0; c < kNB; ++c) a[0][c] = pr[c];
       }
-      const float pv = xrow[1][j];
+      const float pv = pr[j];
       if (pv != 0.f) {
         const float rcp = 1.0f / pv;
-        float pr[kNB];
-#pragma unroll
-        for (int c = 0; c < kNB; ++c) pr[c] = xrow[1][c];
 #pragma unroll
         for (int m = 0; m < M; ++m) {
           const int r = tid + kLuThreads * m;
@@ -248,7 +265,6 @@ __global__ __launch_bounds__(NT, NT <= 256 ? 2 : 1) void lu_panel_kernel(int N, 
           }
         }
       }
-      __syncthreads();  // xrow is rewritten by the next column
     }
   }
 
@@ -405,6 +421,81 @@ __global__ __launch_bounds__(256) void lu_update_block_kernel(int N, int k0, int
       Ab[(size_t)(r0 + r) * N + c0 + c] = v;
     }
   }
+}
+
+// The same update when the half's remaining width is exactly W (a multiple of 16; N % 4 == 0 and
+// 16-B aligned rows): 16-B accesses, and only as many threads per row as the width needs (the
+// generic kernel sizes every launch for the widest update and clamps the rest onto repeated
+// loads).  Same operations in the same order per element as lu_update_block_kernel.
+template <int NB, int W>
+__global__ __launch_bounds__(256) void lu_update_block_vec_kernel(int N, int k0, float* A) {
+  constexpr int kW4 = W / 4, kNB4 = NB / 4;
+  constexpr int kAq = kUpdRows * kW4 / 256;              // float4 of A per thread
+  constexpr int kUq = (NB * kW4 + 255) / 256;             // float4 of U12 per thread
+  constexpr int kLq = (kUpdRows * kNB4 + 255) / 256;      // float4 of L21 per thread
+  static_assert(kAq * 256 == kUpdRows * kW4, "W must be a multiple of 16");
+  __shared__ __attribute__((aligned(16))) float Us[NB][W];
+  __shared__ float Ls[kUpdRows][NB + 1];
+  const int tid = threadIdx.x;
+  float* Ab = A + blockIdx.x * (size_t)N * N;
+  const int c0 = k0 + NB;
+  const int r0 = c0 + blockIdx.y * kUpdRows;
+  const int rows = min(kUpdRows, N - r0);
+  float4 u[kUq], l[kLq], a[kAq];
+#pragma unroll
+  for (int q = 0; q < kUq; ++q) {
+    const int idx = min(tid + 256 * q, NB * kW4 - 1), li = idx / kW4, c = (idx % kW4) * 4;
+    u[q] = *reinterpret_cast<const float4*>(Ab + (size_t)(k0 + li) * N + c0 + c);
+  }
+#pragma unroll
+  for (int q = 0; q < kLq; ++q) {
+    const int idx = min(tid + 256 * q, kUpdRows * kNB4 - 1), r = min(idx / kNB4, rows - 1), li = (idx % kNB4) * 4;
+    l[q] = *reinterpret_cast<const float4*>(Ab + (size_t)(r0 + r) * N + k0 + li);
+  }
+#pragma unroll
+  for (int q = 0; q < kAq; ++q) {
+    const int idx = tid + 256 * q, r = min(idx / kW4, rows - 1), c = (idx % kW4) * 4;
+    a[q] = *reinterpret_cast<const float4*>(Ab + (size_t)(r0 + r) * N + c0 + c);
+  }
+#pragma unroll
+  for (int q = 0; q < kUq; ++q) {
+    const int idx = tid + 256 * q;
+    if (idx < NB * kW4) *reinterpret_cast<float4*>(&Us[idx / kW4][(idx % kW4) * 4]) = u[q];
+  }
+#pragma unroll
+  for (int q = 0; q < kLq; ++q) {
+    const int idx = tid + 256 * q;
+    if (idx < kUpdRows * kNB4) {
+      float* d = &Ls[idx / kNB4][(idx % kNB4) * 4];
+      d[0] = l[q].x; d[1] = l[q].y; d[2] = l[q].z; d[3] = l[q].w;
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int q = 0; q < kAq; ++q) {
+    const int idx = tid + 256 * q, r = idx / kW4, c = (idx % kW4) * 4;
+    if (r < rows) {
+      float4 v = a[q];
+#pragma unroll
+      for (int li = 0; li < NB; ++li) {
+        const float lv = Ls[r][li];
+        const float4 uv = *reinterpret_cast<const float4*>(&Us[li][c]);
+        v.x = v.x - lv * uv.x; v.y = v.y - lv * uv.y; v.z = v.z - lv * uv.z; v.w = v.w - lv * uv.w;
+      }
+      *reinterpret_cast<float4*>(Ab + (size_t)(r0 + r) * N + c0 + c) = v;
+    }
+  }
+}
+
+// In-half update after the panel at k0 (rank NB on the half's columns [k0 + NB, cend)).
+template <int NB>
+static void lu_update_block(int64_t B, int64_t N, int k0, int cend, float* A, bool vec, hipStream_t s) {
+  const int c0 = k0 + NB, w = cend - c0;
+  const dim3 grid((unsigned)B, (unsigned)((N - c0 + kUpdRows - 1) / kUpdRows));
+  if (vec && w == 48) hipLaunchKernelGGL((lu_update_block_vec_kernel<NB, 48>), grid, dim3(256), 0, s, (int)N, k0, A);
+  else if (vec && w == 32) hipLaunchKernelGGL((lu_update_block_vec_kernel<NB, 32>), grid, dim3(256), 0, s, (int)N, k0, A);
+  else if (vec && w == 16) hipLaunchKernelGGL((lu_update_block_vec_kernel<NB, 16>), grid, dim3(256), 0, s, (int)N, k0, A);
+  else hipLaunchKernelGGL(lu_update_block_kernel<NB>, grid, dim3(256), 0, s, (int)N, k0, cend, A);
 }
 
 // The net row permutation of the interchanges of rows [K0, cend) (a 64-column half or, composed, a
@@ -1145,6 +1236,7 @@ using namespace iadmm;
 
 // Panels (+ in-block updates) of the 64-column half [K0, cend).
 static int lu_factor_half(int64_t B, int64_t N, int K0, int cend, float* A, int* piv, int* info, hipStream_t s) {
+  const bool vec = (N % 4 == 0) && aligned16(A);
   if (N <= kPanelMaxM * kLuThreads) {
     for (int k0 = K0; k0 < cend; k0 += kNB) {
       const int R = (int)N - k0;
@@ -1152,12 +1244,12 @@ static int lu_factor_half(int64_t B, int64_t N, int K0, int cend, float* A, int*
       if (R <= kLuThreads) hipLaunchKernelGGL((lu_panel_kernel<1, kNB, kLuThreads>), g, t, 0, s, (int)N, K0, k0, cend, A, piv, info);
       else if (R <= 2 * kLuThreads) hipLaunchKernelGGL((lu_panel_kernel<2, kNB, kLuThreads>), g, t, 0, s, (int)N, K0, k0, cend, A, piv, info);
       else if (R <= 4 * kLuThreads) hipLaunchKernelGGL((lu_panel_kernel<4, kNB, kLuThreads>), g, t, 0, s, (int)N, K0, k0, cend, A, piv, info);
+      else if (R <= 6 * kLuThreads) hipLaunchKernelGGL((lu_panel_kernel<6, kNB, kLuThreads>), g, t, 0, s, (int)N, K0, k0, cend, A, piv, info);
       else hipLaunchKernelGGL((lu_panel_kernel<kPanelMaxM, kNB, kLuThreads>), g, t, 0, s, (int)N, K0, k0, cend, A, piv, info);
       IADMM_CHECK_LAUNCH();
       const int c0 = k0 + kNB;
       if (c0 < cend) {
-        const dim3 grid((unsigned)B, (unsigned)((N - c0 + kUpdRows - 1) / kUpdRows));
-        hipLaunchKernelGGL(lu_update_block_kernel<kNB>, grid, dim3(256), 0, s, (int)N, k0, cend, A);
+        lu_update_block<kNB>(B, N, k0, cend, A, vec, s);
         IADMM_CHECK_LAUNCH();
       }
     }
@@ -1174,8 +1266,7 @@ static int lu_factor_half(int64_t B, int64_t N, int K0, int cend, float* A, int*
       IADMM_CHECK_LAUNCH();
       const int c0 = k0 + kBigNB;
       if (c0 < cend) {
-        const dim3 grid((unsigned)B, (unsigned)((N - c0 + kUpdRows - 1) / kUpdRows));
-        hipLaunchKernelGGL(lu_update_block_kernel<kBigNB>, grid, dim3(256), 0, s, (int)N, k0, cend, A);
+        lu_update_block<kBigNB>(B, N, k0, cend, A, vec, s);
         IADMM_CHECK_LAUNCH();
       }
     }

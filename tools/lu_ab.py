@@ -55,10 +55,14 @@ def child(args):
     berr = (res.norm(dim=1) / (K.flatten(1).norm(dim=1) * xd.norm(dim=1))).max().item()
     N = args.N
     ms = min(times)
+    # bitwise fingerprint of the factors (A/B variants that claim the same arithmetic must agree)
+    lu_sum = sum(int(torch.sum(LU[i:i + 64].view(torch.int32), dtype=torch.int64)) for i in range(0, B, 64))
+    piv_sum = int(torch.sum(piv, dtype=torch.int64))
     print(json.dumps({"lib": os.environ.get("IADMM_LIB_PATH", "default"), "B": B, "N": N, "factor_ms": times,
                       "best_ms": ms, "tflops": B * 2.0 / 3.0 * N ** 3 / ms / 1e9, "frac_fp32_mfma": B * 2.0 / 3.0 * N ** 3 / ms / 1e9 / 157.3,
                       "info_max": int(info.max()), "solve_ms": solve_ms,
-                      "solve_tbps": B * args.N * args.N * 4 / min(solve_ms) / 1e9, "backward_error": berr, "piv_head": piv[0, :8].tolist()}), flush=True)
+                      "solve_tbps": B * args.N * args.N * 4 / min(solve_ms) / 1e9, "backward_error": berr, "piv_head": piv[0, :8].tolist(),
+                      "lu_bits_sum": lu_sum, "piv_sum": piv_sum}), flush=True)
 
 
 def main():

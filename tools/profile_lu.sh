@@ -12,6 +12,7 @@ mkdir -p "$out"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$raw/trace" -o run -- python3 tools/profile_lu.py --batch $B --N $N \
   > "$out/trace.log" 2>&1
 cp "$(find "$raw/trace" -name "*kernel_stats.csv" | head -1)" "$out/${tag}_stage2_kernel_stats_N${N}_B${B}.csv"
+cp "$(find "$raw/trace" -name "*kernel_trace.csv" | head -1)" "$out/${tag}_stage2_kernel_trace_N${N}_B${B}.csv"
 for ctr in FETCH_SIZE WRITE_SIZE; do
   timeout -s KILL 300 rocprofv3 --pmc $ctr --output-format csv -d "$raw/pmc_$ctr" -o run -- \
     python3 tools/profile_lu.py --batch $B --N $N > "$out/pmc_$ctr.log" 2>&1
