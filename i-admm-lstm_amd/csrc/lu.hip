@@ -9,7 +9,8 @@
 //                          half's other columns (?laswp), and U = L11^-1 A is solved for the
 //                          panel rows inside the current half; lu_panel_global_kernel is the
 //                          same column steps with the panel in HBM / L2 (more than 10240 rows).
-//   lu_update_block_kernel A -= L21 U12 on the columns of the current half right of the panel.
+//   lu_update_block_kernel A -= L21 U12 on the columns of the current half right of the panel
+//                          (lu_update_block_vec_kernel<NB, W> when the width is 48, 32 or 16).
 // per 128-column block: first half factored; its interchanges + U12 on the second half
 // (lu_swap_kernel<64, true>); the second half's rank-64 update (lu_trail_kernel, cmax); second
 // half factored; its interchanges on the first half; the block's 128 interchanges composed into
