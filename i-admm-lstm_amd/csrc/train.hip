@@ -173,27 +173,53 @@ __global__ __launch_bounds__(256, 2) void lstm_cell_bwd_kernel(CellBwdArgs a) {
                                  rg = rs(a.g + rbase, nvalid * 4), rdq = rs(a.dq + rbase, nvalid * 4),
                                  rin = rs(a.inpart + ((int64_t)jt * M + rbase) * 2, nvalid * 8);
     const bool full = (jt + 1) * kJT <= h;
+    // Eight steps (r, qq), software-pipelined by one: the loads of step st + 1 are issued before the
+    // stores of step st.  vmcnt counts stores as well as loads and retires them in issue order, so a
+    // load issued after a store cannot be waited for without waiting for that store's write
+    // acknowledgement too: loading at the top of each step (r03 first form) put every step's five
+    // stores (dC, 4 x dP) in front of the next step's loads (rocprof A/B: the stores alone were
+    // 1.2 of 10.4 ms per launch).  sched_barrier(0)s pin that order.
+    unsigned vr[2], vo[2], vp[2];
+    bool rok[2];
 #pragma unroll
     for (int r = 0; r < 2; ++r) {
       const int row = wave * 64 + r * 32 + jl;
-      const bool rok = row < nvalid;
-      const unsigned vr = (unsigned)row * 4u;
-      const unsigned vo = ((unsigned)row * (unsigned)h + (unsigned)(jt * kJT + 4 * hf)) * 4u;
-      const unsigned vp = ((unsigned)row * (unsigned)(4 * h) + (unsigned)(jt * kJT + 4 * hf)) * 4u;
-      const float2v in0 = splat2(__uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rxv, vr, 0, 0)));
-      const float2v in1 = splat2(__uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rg, vr, 0, 0)));
-      const float2v dqv = splat2(__uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rdq, vr, 0, 0)));
-      float2v din0 = splat2(0.f), din1 = splat2(0.f);
+      rok[r] = row < nvalid;
+      vr[r] = (unsigned)row * 4u;
+      vo[r] = ((unsigned)row * (unsigned)h + (unsigned)(jt * kJT + 4 * hf)) * 4u;
+      vp[r] = ((unsigned)row * (unsigned)(4 * h) + (unsigned)(jt * kJT + 4 * hf)) * 4u;
+    }
+    float4 ldv[8][3];
+    float rsc[2][3];
+    auto qa_of = [&](int qq) -> unsigned {
+      const bool uok = full || jt * kJT + 8 * qq + 4 * hf < h;
+      return uok ? 32u * qq : 0x80000000u;
+    };
+    auto issue = [&](int st) {
+      const int r = st >> 2, qq = st & 3;
+      if (qq == 0) {
+        rsc[r][0] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rxv, vr[r], 0, 0));
+        rsc[r][1] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rg, vr[r], 0, 0));
+        rsc[r][2] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rdq, vr[r], 0, 0));
+      }
+      const unsigned qa = qa_of(qq);
+      ldv[st][0] = u2f4(__builtin_amdgcn_raw_buffer_load_b128(rC, vo[r] + qa, 0, 0));
+      ldv[st][1] = u2f4(__builtin_amdgcn_raw_buffer_load_b128(rdH, vo[r] + qa, 0, 0));
+      ldv[st][2] = u2f4(__builtin_amdgcn_raw_buffer_load_b128(rdCn, vo[r] + qa, 0, 0));
+    };
+    issue(0);
+    float2v din0 = splat2(0.f), din1 = splat2(0.f);
 #pragma unroll
-      for (int qq = 0; qq < 4; ++qq) {
-        __builtin_amdgcn_sched_barrier(0);
+    for (int st = 0; st < 8; ++st) {
+      __builtin_amdgcn_sched_barrier(0);
+      const int r = st >> 2, qq = st & 3;
+      const float2v in0 = splat2(rsc[r][0]), in1 = splat2(rsc[r][1]), dqv = splat2(rsc[r][2]);
+      if (qq == 0) { din0 = splat2(0.f); din1 = splat2(0.f); }
+      {
         const int jj0 = 8 * qq + 4 * hf;
         const bool uok = full || jt * kJT + jj0 < h;
-        const bool ok4 = rok && uok;
-        const unsigned qa = uok ? 32u * qq : 0x80000000u;
-        const float4 cin4 = u2f4(__builtin_amdgcn_raw_buffer_load_b128(rC, vo + qa, 0, 0));
-        const float4 dh4 = u2f4(__builtin_amdgcn_raw_buffer_load_b128(rdH, vo + qa, 0, 0));
-        const float4 dc4 = u2f4(__builtin_amdgcn_raw_buffer_load_b128(rdCn, vo + qa, 0, 0));
+        const bool ok4 = rok[r] && uok;
+        const float4 cin4 = ldv[st][0], dh4 = ldv[st][1], dc4 = ldv[st][2];
         float4 dC4, dP4[4];
 #pragma unroll
         for (int pp = 0; pp < 2; ++pp) {
@@ -244,17 +270,23 @@ __global__ __launch_bounds__(256, 2) void lstm_cell_bwd_kernel(CellBwdArgs a) {
             din1 += ((dPi * fld(1) + dPf * fld(4)) + dPo * fld(7)) + dPu * fld(10);
           }
         }
-        __builtin_amdgcn_raw_buffer_store_b128(f42u(dC4), rdC, vo + qa, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+        if (st + 1 < 8) issue(st + 1);
+        __builtin_amdgcn_sched_barrier(0);
+        const unsigned qa = qa_of(qq);
+        __builtin_amdgcn_raw_buffer_store_b128(f42u(dC4), rdC, vo[r] + qa, 0, 0);
 #pragma unroll
         for (int g = 0; g < 4; ++g)
-          __builtin_amdgcn_raw_buffer_store_b128(f42u(dP4[g]), rdP, vp + (unsigned)(g * h * 4) + qa, 0, 0);
+          __builtin_amdgcn_raw_buffer_store_b128(f42u(dP4[g]), rdP, vp[r] + (unsigned)(g * h * 4) + qa, 0, 0);
       }
-      float d0 = din0.x + din0.y, d1 = din1.x + din1.y;
-      d0 += __shfl_xor(d0, 32, 64);
-      d1 += __shfl_xor(d1, 32, 64);
-      const unsigned vi = hf ? 0x80000000u : (unsigned)row * 8u;
-      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(d0), rin, vi, 0, 0);
-      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(d1), rin, vi + 4u, 0, 0);
+      if (qq == 3) {
+        float d0 = din0.x + din0.y, d1 = din1.x + din1.y;
+        d0 += __shfl_xor(d0, 32, 64);
+        d1 += __shfl_xor(d1, 32, 64);
+        const unsigned vi = hf ? 0x80000000u : vr[r] * 2u;
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(d0), rin, vi, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(d1), rin, vi + 4u, 0, 0);
+      }
     }
   } else {
 #pragma unroll
