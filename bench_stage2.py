@@ -48,6 +48,8 @@ def main():
     ap.add_argument("--steps", type=int, default=2)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--cpu-sample", type=int, default=2)
+    ap.add_argument("--chunk", type=int, default=0,
+                    help="instances per factorisation chunk (0: solver.stage2_chunk, balanced under the memory cap)")
     args = ap.parse_args()
     from iadmm import data, ops, solver
     n, mi, me, B = args.num_var, args.num_ineq, args.num_eq, args.batch
@@ -65,7 +67,7 @@ def main():
                 d["zu"].reshape(B, m).contiguous(), rho, x, y, z, 6e-6, args.iters)
 
     def step(timer):
-        return solver.stage2(*args_dev, timer=timer)
+        return solver.stage2(*args_dev, timer=timer, chunk=args.chunk or None)
 
     for _ in range(args.warmup):
         out = step(None)

@@ -366,7 +366,17 @@ def stage2_chunk(B, N, budget_bytes=None):
         cached = torch.cuda.memory_reserved() - torch.cuda.memory_allocated()
         budget_bytes = int(0.8 * (free + cached))
     per = 4 * N * N + 64 * N  # K (factored in place) + pivots, rhs, solution, iterates
-    return max(1, min(B, budget_bytes // per))
+    cap = max(1, min(B, budget_bytes // per))
+    # equal chunks, rounded up to whole multiples of the CU count when that adds no chunk: the
+    # panel kernels run one workgroup per instance, so 512 instances as 410 + 102 take three
+    # rounds of panels per column and as 256 + 256 two (the other kernels are throughput-bound)
+    nch = -(-B // cap)
+    step = -(-B // nch)
+    cus = torch.cuda.get_device_properties(torch.cuda.current_device()).multi_processor_count \
+        if torch.cuda.is_available() else 0
+    if cus and step > cus and -(-step // cus) * cus <= cap:
+        step = -(-step // cus) * cus
+    return step
 
 
 def stage2(Q, p, A0, zl, zu, rho_rows, x, y, z, sigma, iters, alpha=STAGE2_ALPHA, timer=None, iter_hook=None,

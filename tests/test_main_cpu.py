@@ -29,3 +29,15 @@ def test_timed_seconds_sums_only_the_reference_timed_spans():
     counted = {k for k in spans if main.timed_seconds({k: spans[k]}) > 0}
     assert counted == TIMED & names, counted
     assert main.timed_seconds(spans) == len(TIMED & names)
+
+
+def test_stage2_chunks_are_balanced():
+    """solver.stage2_chunk: equal chunks under the memory cap (config 4: 512 instances whose dense
+    K fit 410 at a time run as 256 + 256, not 410 + 102); the whole batch when it fits."""
+    from iadmm import solver
+    per = lambda N: 4 * N * N + 64 * N  # noqa: E731
+    assert solver.stage2_chunk(512, 10000, budget_bytes=410 * per(10000)) == 256
+    assert solver.stage2_chunk(1024, 2000, budget_bytes=2000 * per(2000)) == 1024
+    assert solver.stage2_chunk(5, 100, budget_bytes=2 * per(100)) == 2
+    assert solver.stage2_chunk(7, 100, budget_bytes=3 * per(100)) == 3
+    assert solver.stage2_chunk(3, 100, budget_bytes=0) == 1
