@@ -531,10 +531,18 @@ __global__ __launch_bounds__(256) void lu_swap_kernel(int N, int K0, int nbk, in
   const int tid = threadIdx.x;
   const size_t b = blockIdx.x;
   float* Ab = A + b * (size_t)N * N;
-  if constexpr (TRSM) {
-    for (int idx = tid; idx < kBlk * kBlk; idx += blockDim.x) {
-      const int r = idx / kBlk, c = idx % kBlk;
-      Ld[r][c] = Ab[(size_t)(K0 + r) * N + K0 + c];
+  if constexpr (TRSM) {  // (256 threads: the 64 x 64 block's 16 loads per thread all in flight at once)
+    constexpr int kLq = kBlk * kBlk / 256;
+    float lv[kLq];
+#pragma unroll
+    for (int q = 0; q < kLq; ++q) {
+      const int idx = tid + 256 * q, r = idx / kBlk, c = idx % kBlk;
+      lv[q] = Ab[(size_t)(K0 + r) * N + K0 + c];
+    }
+#pragma unroll
+    for (int q = 0; q < kLq; ++q) {
+      const int idx = tid + 256 * q;
+      Ld[idx / kBlk][idx % kBlk] = lv[q];
     }
   }
   const int* pb = perm + b * kPermInts;
@@ -763,9 +771,22 @@ __global__ __launch_bounds__(kOB) void lu_linv_kernel(int N, int P, const float*
   const int j = threadIdx.x;
   const size_t b = blockIdx.x;
   const float* Ab = A + b * (size_t)N * N;
-  for (int idx = j; idx < kOB * kOB; idx += blockDim.x) {
-    const int r = idx / kOB, c = idx % kOB;
-    L[r][c] = c < r ? Ab[(size_t)(P + r) * N + P + c] : 0.f;
+  // the 128 x 128 block in four batches of 32 row loads per thread (a batch's loads all in flight
+  // together; r03 first form: a 128-iteration load -> LDS-store loop, one latency after another)
+  constexpr int kLB = 32;
+#pragma unroll
+  for (int h0 = 0; h0 < kOB * kOB; h0 += kLB * kOB) {
+    float v[kLB];
+#pragma unroll
+    for (int i = 0; i < kLB; ++i) {
+      const int idx = h0 + i * kOB + j, r = idx / kOB, c = idx % kOB;
+      v[i] = Ab[(size_t)(P + r) * N + P + c];
+    }
+#pragma unroll
+    for (int i = 0; i < kLB; ++i) {
+      const int idx = h0 + i * kOB + j, r = idx / kOB, c = idx % kOB;
+      L[r][c] = c < r ? v[i] : 0.f;
+    }
   }
   __syncthreads();
   float x[kOB];
