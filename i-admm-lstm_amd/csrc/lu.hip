@@ -1104,8 +1104,11 @@ constexpr int kDS = kSolveBlk + 1;  // LDS stride of the staged diagonal block
 #define IADMM_SOLVE_LAZY_PIV 1
 #endif
 // VEC (N % 4 == 0, 16-B aligned factors): block bounds are multiples of 4, rows 16-B aligned.
-template <bool VEC>
-__global__ __launch_bounds__(kSolveThreads, 4) void lu_solve_kernel(int N, const float* LU, const int* piv,
+// NT threads per workgroup: 256 (4 workgroups per CU) when the batch fills the CUs four times
+// over, 512 / 1024 for smaller batches (config 4's 256-instance chunks: one workgroup per CU, so
+// 16 waves instead of 4 stream its rows; the block loop spreads over any number of waves).
+template <bool VEC, int NT = kSolveThreads>
+__global__ __launch_bounds__(NT, NT == 256 ? 4 : (NT == 512 ? 2 : 1)) void lu_solve_kernel(int N, const float* LU, const int* piv,
                                                               float* X) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   float* x = sm;                  // N
@@ -1116,7 +1119,7 @@ __global__ __launch_bounds__(kSolveThreads, 4) void lu_solve_kernel(int N, const
   const float* M = LU + b * (size_t)N * N;
   float* xb = X + b * N;
 #pragma unroll 8
-  for (int i = tid; i < N; i += kSolveThreads) x[i] = xb[i];
+  for (int i = tid; i < N; i += NT) x[i] = xb[i];
   __syncthreads();
   if (!IADMM_SOLVE_LAZY_PIV && wave == 0) {  // all interchanges up front, 64 pivots per load
     for (int i0 = 0; i0 < N; i0 += 64) {
@@ -1142,17 +1145,17 @@ __global__ __launch_bounds__(kSolveThreads, 4) void lu_solve_kernel(int N, const
       const int nbk = k1 - k0;
       // the diagonal block: every thread issues its loads at once (clamped, valid addresses; the
       // entries past nbk are never read), the LDS writes after the dot products below
-      constexpr int kDQ = kSolveBlk * kSolveBlk / kSolveThreads;
+      constexpr int kDQ = kSolveBlk * kSolveBlk / NT;
       {
         float dreg[kDQ];
 #pragma unroll
         for (int q = 0; q < kDQ; ++q) {
-          const int idx = tid + kSolveThreads * q, r = min(idx / kSolveBlk, nbk - 1), c = min(idx % kSolveBlk, nbk - 1);
+          const int idx = tid + NT * q, r = min(idx / kSolveBlk, nbk - 1), c = min(idx % kSolveBlk, nbk - 1);
           dreg[q] = M[(size_t)(k0 + r) * N + k0 + c];
         }
 #pragma unroll
         for (int q = 0; q < kDQ; ++q) {
-          const int idx = tid + kSolveThreads * q;
+          const int idx = tid + NT * q;
           D[(idx / kSolveBlk) * kDS + idx % kSolveBlk] = dreg[q];
         }
       }
@@ -1230,7 +1233,7 @@ __global__ __launch_bounds__(kSolveThreads, 4) void lu_solve_kernel(int N, const
     }
   }
 #pragma unroll 8
-  for (int i = tid; i < N; i += kSolveThreads) xb[i] = x[i];
+  for (int i = tid; i < N; i += NT) xb[i] = x[i];
 }
 
 // b~ = [sigma x - p ; z - y / rho]  (models/lu.py:125,129)
@@ -1416,7 +1419,17 @@ extern "C" int iadmm_lu_solve(int64_t B, int64_t N, const float* LU, const int* 
   if (lds > 160 * 1024 || B > 0x7fffffff) return IADMM_E_SIZE;  // gfx950: 160 KiB of LDS per workgroup
   IADMM_ALLOW_LDS(lu_solve_kernel<true>, lds);
   IADMM_ALLOW_LDS(lu_solve_kernel<false>, lds);
-  if (N % 4 == 0 && aligned16(LU))
+  int dev = 0, cus = 256;
+  if (hipGetDevice(&dev) == hipSuccess) hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  IADMM_ALLOW_LDS((lu_solve_kernel<true, 512>), lds);
+  IADMM_ALLOW_LDS((lu_solve_kernel<true, 1024>), lds);
+  if (N % 4 == 0 && aligned16(LU) && B <= cus)
+    hipLaunchKernelGGL((lu_solve_kernel<true, 1024>), dim3((unsigned)B), dim3(1024), lds, (hipStream_t)stream,
+                       (int)N, LU, piv, x);
+  else if (N % 4 == 0 && aligned16(LU) && B <= 2 * cus)
+    hipLaunchKernelGGL((lu_solve_kernel<true, 512>), dim3((unsigned)B), dim3(512), lds, (hipStream_t)stream,
+                       (int)N, LU, piv, x);
+  else if (N % 4 == 0 && aligned16(LU))
     hipLaunchKernelGGL(lu_solve_kernel<true>, dim3((unsigned)B), dim3(kSolveThreads), lds, (hipStream_t)stream,
                        (int)N, LU, piv, x);
   else
