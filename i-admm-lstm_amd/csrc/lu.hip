@@ -595,7 +595,10 @@ __global__ __launch_bounds__(256) void lu_swap_kernel(int N, int K0, int nbk, in
 // strips of one instance are consecutive logical ids on one XCD (its L2 serves the -L21 re-reads
 // of the 16 strips).  VEC: N % 4 == 0 and 16-B aligned rows (16-B global accesses).
 // DIAG (tools/lubench.hip only): 1 = no MFMAs (the memory pipeline alone).
-template <bool VEC, int DIAG = 0>
+// TCW = 64 (the mid update, whose strip is the block's second half only): the loads, stores and
+// U12 staging cover 64 columns and the waves of columns 64..127 skip their MFMAs (r03: the full
+// 128-column mapping loaded and zero-masked the other half, twice the A22 reads).
+template <bool VEC, int DIAG = 0, int TCW = kTC>
 __global__ __launch_bounds__(kTrailThreads, 1) void lu_trail_kernel(int N, int K0, int ntc, int nrc, int cmax,
                                                                       float* A) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
@@ -619,10 +622,10 @@ __global__ __launch_bounds__(kTrailThreads, 1) void lu_trail_kernel(int N, int K
 
   typedef typename std::conditional<VEC, float4, float>::type VT;
   constexpr int W = VEC ? 4 : 1;                    // floats per global access
-  constexpr int kCQ = kTRS * kTC / W / NT;          // A22 accesses per thread per step
+  constexpr int kCQ = kTRS * TCW / W / NT;          // A22 accesses per thread per step
   constexpr int kLQ = kTRS * kBlk / W / NT;         // -L21 accesses per thread per step
-  constexpr int kUQ = kBlk * kTC / W / NT;          // U12 accesses per thread
-  constexpr int CPR = kTC / W, LPR = kBlk / W;      // accesses per row
+  constexpr int kUQ = kBlk * TCW / W / NT;          // U12 accesses per thread
+  constexpr int CPR = TCW / W, LPR = kBlk / W;      // accesses per row
   auto ld = [&](int row, int col, bool ok) -> VT {  // clamped address, masked value
     const float* p = Ab + (size_t)row * N + col;
     if constexpr (VEC) {
@@ -712,7 +715,7 @@ __global__ __launch_bounds__(kTrailThreads, 1) void lu_trail_kernel(int N, int K
       loadC(step + 1, cr);
       loadL(step + 1, lr);
     }
-    if constexpr (DIAG != 1) {
+    if (DIAG != 1 && (TCW == kTC || wc < TCW)) {
       const float* Ls = Lsb + (step & 1) * kTRS * kTS;
 #pragma unroll
       for (int sg = 0; sg < 8; ++sg) {
@@ -1329,7 +1332,9 @@ static int lu_rank64(int64_t B, int64_t N, int K0, int cend, int cmax, float* A,
   if (rest <= 0 || wid <= 0) return 0;
   const int ntc = (wid + kTC - 1) / kTC, nrc = (rest + kTRW - 1) / kTRW;
   const dim3 grid((unsigned)(B * ntc * nrc));
-  if (vec) hipLaunchKernelGGL(lu_trail_kernel<true>, grid, dim3(kTrailThreads), kTrailLds, s, (int)N, K0, ntc, nrc, cmax, A);
+  if (vec && wid <= kTC / 2)
+    hipLaunchKernelGGL((lu_trail_kernel<true, 0, kTC / 2>), grid, dim3(kTrailThreads), kTrailLds, s, (int)N, K0, ntc, nrc, cmax, A);
+  else if (vec) hipLaunchKernelGGL(lu_trail_kernel<true>, grid, dim3(kTrailThreads), kTrailLds, s, (int)N, K0, ntc, nrc, cmax, A);
   else hipLaunchKernelGGL(lu_trail_kernel<false>, grid, dim3(kTrailThreads), kTrailLds, s, (int)N, K0, ntc, nrc, cmax, A);
   IADMM_CHECK_LAUNCH();
   return 0;
@@ -1343,6 +1348,7 @@ static int lu_factor_blocks(int64_t B, int64_t N, float* A, int* piv, int* info,
                             hipStream_t s) {
   const bool vec = (N % 4 == 0) && aligned16(A);
   IADMM_ALLOW_LDS(lu_trail_kernel<true>, kTrailLds);
+  IADMM_ALLOW_LDS((lu_trail_kernel<true, 0, kTC / 2>), kTrailLds);
   IADMM_ALLOW_LDS(lu_trail_kernel<false>, kTrailLds);
   IADMM_ALLOW_LDS(lu_trail128_kernel<true>, kT2Lds);
   IADMM_ALLOW_LDS(lu_trail128_kernel<false>, kT2Lds);
