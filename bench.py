@@ -84,23 +84,25 @@ def pmc_traffic(kernel_prefix, n, m, h, B, lanes=1):
     committed rocprofv3 --pmc summaries of this exact workload (tools/pmc_summary.py output, one
     FETCH_SIZE and one WRITE_SIZE pass; file suffix ``_L{lanes}`` when lanes > 1).
     gfx950 correction (MI355X_MICROARCH.md §HBM): FETCH_SIZE counts 128-B requests at 64 B, so
-    it is doubled; WRITE_SIZE is taken as is.  Returns None when no matching profile exists."""
+    it is doubled; WRITE_SIZE is taken as is.  Returns (bytes, [the profile files used]), or
+    (None, None) when no matching profile exists."""
     import csv
     import glob
-    tot = 0.0
+    tot, used = 0.0, []
     for ctr, mult in (("FETCH_SIZE", 2.0), ("WRITE_SIZE", 1.0)):
         sfx = f"_L{lanes}" if lanes > 1 else ""
         files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_pmc_{ctr}_n{n}_m{m}_h{h}_B{B}{sfx}.csv")))
         if not files:
-            return None
+            return None, None
         names = (kernel_prefix,) if isinstance(kernel_prefix, str) else kernel_prefix
         rows = [r for r in csv.DictReader(open(files[-1]))
                 if any(k in r["kernel"] for k in names) and r["counter"] == ctr]
         if not rows:
-            return None
+            return None, None
         # one launch of the operation = one dispatch of every kernel it consists of
         tot += mult * sum(float(r["mean"]) for r in rows) * 1024.0 * lanes
-    return tot
+        used.append(os.path.relpath(files[-1], ROOT))
+    return tot, used
 
 
 def rocprof_avg_ms(kernels, tag_glob="r*_bench_kernel_stats.csv"):
@@ -125,21 +127,69 @@ def pmc_traffic_stage2(n, m, B):
     """HBM bytes of one factorization (every lu_* kernel but the solve) from the committed Stage-II
     PMC summaries of tools/profile_lu.py (one factorization; tools/pmc_summary.py: per-kernel mean
     per dispatch x dispatches), FETCH_SIZE x 2
-    (gfx950 correction) + WRITE_SIZE; None without a matching profile."""
+    (gfx950 correction) + WRITE_SIZE; (bytes, [files used]) or (None, None) without a matching
+    profile."""
     import csv
     import glob
-    tot = 0.0
+    tot, used = 0.0, []
     for ctr, mult in (("FETCH_SIZE", 2.0), ("WRITE_SIZE", 1.0)):
         files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_stage2_pmc_{ctr}_N{n + m}_B{B}.csv")))
         if not files:
-            return None
+            return None, None
         rows = [r for r in csv.DictReader(open(files[-1]))
                 if "iadmm::lu_" in r["kernel"] and "solve" not in r["kernel"] and r["counter"] == ctr]
         if not rows:
-            return None
+            return None, None
         # the profile run factors once (tools/profile_lu.py): every dispatch belongs to it
         tot += mult * sum(float(r["mean"]) * float(r["dispatches"]) for r in rows) * 1024.0
-    return tot
+        used.append(os.path.relpath(files[-1], ROOT))
+    return tot, used
+
+
+def box_ceiling(local):
+    """What THIS box delivers: the fp32 MFMA rate of a register-only
+    v_mfma_f32_32x32x2_f32 stream on every SIMD (csrc/probe.hip, 2 workgroups of 4 waves per CU,
+    ~40 ms per run, best of 3) and the HBM rate of a 1-GiB float4 copy (2 x bytes per launch,
+    best of 10), both timed with hipEvents on the launch stream before the timed steps.  The
+    rooflines report their fraction of these beside the fraction of the spec peaks."""
+    from iadmm import _abi, ops
+    cus = torch.cuda.get_device_properties(local).multi_processor_count
+    blocks = 2 * cus
+    out = torch.empty(blocks * 256, dtype=torch.float32, device="cuda")
+    st = torch.cuda.current_stream()
+
+    def timed(fn):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(st)
+        fn()
+        e1.record(st)
+        e1.synchronize()
+        return e0.elapsed_time(e1)
+
+    def mfma(iters):
+        return timed(lambda: _abi.call("iadmm_probe_mfma", blocks, iters, out.data_ptr(), ops._stream()))
+
+    mfma(1000)
+    it = 20000
+    it = max(1000, int(it * 40.0 / max(mfma(it), 1e-3)))
+    flop = float(_abi.lib().iadmm_probe_mfma_flop(blocks, it))
+    tflops = max(flop / (mfma(it) * 1e-3) / 1e12 for _ in range(3))
+    nbytes = 1 << 30
+    src = torch.ones(nbytes // 4, dtype=torch.float32, device="cuda")
+    dst = torch.empty_like(src)
+
+    def copy():
+        return timed(lambda: _abi.call("iadmm_probe_copy", nbytes, src.data_ptr(), dst.data_ptr(), ops._stream()))
+
+    copy()
+    gbs = max(2.0 * nbytes / (copy() * 1e-3) / 1e9 for _ in range(10))
+    ok = bool(torch.equal(dst[:1024], src[:1024]))
+    del src, dst, out
+    torch.cuda.empty_cache()
+    return {"mfma_f32_tflops": tflops, "mfma_frac_of_spec": tflops / FP32_MFMA_PEAK_TFLOPS,
+            "hbm_copy_gbs": gbs, "hbm_frac_of_spec": gbs / HBM_PEAK_GBS, "copy_checked": ok,
+            "method": f"csrc/probe.hip: {blocks} x 256-thread workgroups x {it} x 8 register MFMAs "
+                      f"(v_mfma_f32_32x32x2_f32), best of 3; float4 copy of 1 GiB, best of 10; hipEvents"}
 
 
 def baseline_config(args, world):
@@ -247,15 +297,16 @@ def stage2_record(args, d, out, n, mi, me, B):
     fac_ms = spans.get("stage2_factor")
     fac_flop = B * 2.0 / 3.0 * N ** 3
     fac_tf = fac_flop / (fac_ms * 1e-3) / 1e12
+    st2_traffic, st2_src = pmc_traffic_stage2(n, mi + me, B)
     rec = {"value": B / el, "unit": "QP instances/s", "feas_rest_num": args.stage2_iters, "ms": 1e3 * el,
            "assemble_ms": spans.get("stage2_assemble"), "factor_ms": fac_ms,
            "solve_iter_ms": spans.get("stage2_iterations", 0.0) / args.stage2_iters,
            "roofline": {"kernel": "iadmm_lu_factor", "bound": "mfma", "achieved": fac_tf,
                         "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": fac_tf / FP32_MFMA_PEAK_TFLOPS,
                         "algorithmic_per_launch": fac_flop, "algorithmic": "2/3 N^3 per instance (getrf)",
-                        "traffic": pmc_traffic_stage2(n, mi + me, B),
-                        "traffic_source": "profiles/r*_stage2_pmc_{FETCH,WRITE}_SIZE_N*_B*.csv, all LU kernels "
-                                          "of one factorization (separate --pmc passes)"},
+                        "traffic": st2_traffic, "traffic_source": st2_src,
+                        "traffic_note": "all LU kernels of one factorization (FETCH_SIZE x 2 + WRITE_SIZE, "
+                                        "separate --pmc passes of tools/profile_lu.py)"},
            "chunk": r["chunk"], "final_primal_mean": float(pr[1].mean()), "final_dual_mean": float(pr[2].mean()),
            "note": "Stage II (--feas_rest) on the solved batch: K assembled from the last Stage-I rho on the "
                    "unscaled data, batched blocked LU (csrc/lu.hip) once, feas_rest_num solves + alpha=1.6 "
@@ -388,6 +439,7 @@ def main():
     local, backend = parallel.device_and_backend(local)
     torch.cuda.set_device(local)
     dist = parallel.init(backend, local) if parallel.want_dist(world) else None
+    box = box_ceiling(local)  # before any data is allocated (the copy takes 2 GiB)
 
     n, mi, me, h, T, B = args.num_var, args.num_ineq, args.num_eq, args.hidden_dim, args.outer_T, args.batch
     N = n + mi + me
@@ -423,6 +475,7 @@ def main():
 
     timer = solver.Timer(True)
     elapsed = 0.0
+    step_times = []
     out = None
     for _ in range(args.steps):
         if dist:
@@ -432,8 +485,10 @@ def main():
         t0 = time.perf_counter()
         out = step(timer)
         torch.cuda.synchronize()
-        elapsed += time.perf_counter() - t0
-        print(f"[bench] rank {rank} step done, {time.perf_counter() - t0:.2f} s", file=sys.stderr, flush=True)
+        step_times.append(time.perf_counter() - t0)
+        elapsed += step_times[-1]
+        print(f"[bench] rank {rank} step done, {step_times[-1]:.2f} s", file=sys.stderr, flush=True)
+    elapsed_own = elapsed
     elapsed = parallel.max_over_ranks(elapsed, dist, device="cuda")
     primal, dual = float(out["primal"].mean()), float(out["dual"].mean())
 
@@ -516,6 +571,13 @@ def main():
             gbs = kkt_bytes / (ms_rp * 1e-3) / 1e9
             kkt_rocprof = {"avg_launch_ms": ms_rp, "achieved": gbs, "frac": gbs / HBM_PEAK_GBS, "source": src}
 
+    cell_traffic = pmc_traffic(("cell_fwd_dma_kernel",), n, mi + me, h, B, lanes)
+    kkt_traffic = pmc_traffic(KKT_KERNELS, n, mi + me, h, B, lanes)
+    # per-rank record (which GPU, which instances, how long): gathered to rank 0 (measurement only)
+    ranks = parallel.gather_records(dict(rank=rank, first=first, count=count, elapsed_s=elapsed_own,
+                                         step_s=step_times, box_mfma_tflops=box["mfma_f32_tflops"],
+                                         box_hbm_gbs=box["hbm_copy_gbs"], **parallel.device_record(local)), dist)
+
     res = None
     if rank == 0:
         total = world * B * args.steps
@@ -542,14 +604,13 @@ def main():
                                "weights": weights_tag},
             "roofline": {"kernel": "iadmm_lstm_cell_fwd", "bound": "mfma", "achieved": cell_tf,
                          "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": cell_tf / FP32_MFMA_PEAK_TFLOPS,
-                         "traffic": pmc_traffic(("cell_fwd_dma_kernel",), n, mi + me, h, B, lanes),
-                         "traffic_source": "profiles/r*_pmc_{FETCH,WRITE}_SIZE_*.csv (separate --pmc passes)",
+                         "traffic": cell_traffic[0], "traffic_source": cell_traffic[1],
                          "avg_launch_ms": ms_cell, "launches": n_cell, "busy_ms_per_iteration": busy_cell / iters,
                          "algorithmic_per_iteration": cell_flop,
                          "algorithmic_per_launch": cell_flop / lanes},
             "roofline_matvec": {"kernel": "iadmm_kkt_resgrad", "bound": "hbm", "achieved": kkt_gbs,
                                 "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": kkt_gbs / HBM_PEAK_GBS,
-                                "traffic": pmc_traffic(KKT_KERNELS, n, mi + me, h, B, lanes),
+                                "traffic": kkt_traffic[0], "traffic_source": kkt_traffic[1],
                                 "kernels": "kkt_split_p1 + c1 + p2 + c2 (row-block split, csrc/kkt.hip)",
                                 "timing": "hipEvents around the four launches of each call, this run",
                                 "rocprof": kkt_rocprof,
@@ -558,9 +619,26 @@ def main():
                                 "algorithmic_per_launch": kkt_bytes / lanes},
             "phase_ms_per_step": {k: v / args.steps for k, v in spans.items() if not k.startswith("k:")},
         }
+        # the same fractions against what this box measured before the timed steps (box_ceiling)
+        res["roofline"]["box_ceiling"] = box
+        res["roofline"]["frac_vs_box"] = cell_tf / box["mfma_f32_tflops"]
+        res["roofline_matvec"]["frac_vs_box"] = kkt_gbs / box["hbm_copy_gbs"]
+        per_inst = cell_flop / B * T  # cell flop of one instance's K iterations
+        per_gpu = res["value"] / world
+        res["step_efficiency"] = {
+            "ceiling_spec": FP32_MFMA_PEAK_TFLOPS * 1e12 / per_inst,
+            "ceiling_box": box["mfma_f32_tflops"] * 1e12 / per_inst,
+            "vs_spec": per_gpu / (FP32_MFMA_PEAK_TFLOPS * 1e12 / per_inst),
+            "vs_box": per_gpu / (box["mfma_f32_tflops"] * 1e12 / per_inst),
+            "note": "QP instances/s per GPU against the cell GEMM's ceiling (its flop at the fp32 MFMA spec "
+                    "peak, and at this box's measured MFMA rate)"}
+        res["ranks"] = ranks
+        res["ranks_tile_batch"] = parallel.check_tiling(ranks, world * B)
         if st2 is not None:
+            st2["roofline"]["frac_vs_box"] = st2["roofline"]["achieved"] / box["mfma_f32_tflops"]
             res["stage2"] = st2
         if trn is not None:
+            trn["roofline"]["frac_vs_box"] = trn["roofline"]["achieved"] / box["mfma_f32_tflops"]
             res["train"] = trn
         elif args.train_batch > 0:
             res["train"] = {"skipped": f"one micro-batch of {mb_t} saves {act_bytes / 1e9:.0f} GB of activations "

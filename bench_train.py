@@ -44,6 +44,9 @@ def main():
     ap.add_argument("--outer_T", type=int, default=100)
     ap.add_argument("--steps", type=int, default=2)
     ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--reduce", choices=("ordered", "allreduce"), default="ordered",
+                    help="gradient reduction over ranks (iadmm/train.py): the ordered fold (bitwise "
+                         "world-size invariant) or the ring all-reduce")
     args = ap.parse_args()
     launch_ranks(args)
     from iadmm import data, ops, parallel, train
@@ -63,12 +66,13 @@ def main():
 
     def step():
         return train.tbptt_batch(model, d, mi, me, T, T, 6e-6, opt, micro_batch=args.micro_batch,
-                                 global_batch=world * B, dist=dist)
+                                 global_batch=world * B, dist=dist, reduce=args.reduce)
 
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
     el = 0.0
+    step_s = []
     for _ in range(args.steps):
         if dist:
             dist.barrier()
@@ -76,7 +80,10 @@ def main():
         t0 = time.perf_counter()
         loss = step()
         torch.cuda.synchronize()
-        el += time.perf_counter() - t0
+        step_s.append(time.perf_counter() - t0)
+        el += step_s[-1]
+    ranks = parallel.gather_records(dict(rank=rank, first=first, count=count, elapsed_s=el, step_s=step_s,
+                                         **parallel.device_record(local)), dist)
     el = parallel.max_over_ranks(el, dist, device="cuda")
     if rank == 0:
         N = n + mi + me
@@ -87,7 +94,8 @@ def main():
                           "hidden_dim": h, "loss": loss,
                           "cell_gemm_tflops_equiv": 4 * fwd_flop * args.steps / el / 1e12,
                           "dist_backend": dist.get_backend() if dist else None,
-                          "allreduce_calls": train.ALLREDUCE_CALLS,
+                          "allreduce_calls": train.ALLREDUCE_CALLS, "reduce": args.reduce,
+                          "ranks": ranks, "ranks_tile_batch": parallel.check_tiling(ranks, world * B),
                           "note": "cell GEMM work per step = forward + recompute + dH + dU = 4x forward flops"}))
     if dist:
         dist.destroy_process_group()

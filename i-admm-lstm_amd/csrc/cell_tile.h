@@ -863,9 +863,6 @@ __global__ __launch_bounds__(256, 2) void cell_fwd_dma_kernel(CellArgsT a) {
     a.part[(int64_t)blockIdx.x * 256 + tid] = t;
     return;
   }
-#ifdef IADMM_EPI_PRIO
-  __builtin_amdgcn_s_setprio(IADMM_EPI_PRIO);  // variant study: epilogue priority
-#endif
   uint64_t t_c = 0;
   if constexpr (DIAG >= 4) {
     t_ml = __builtin_amdgcn_s_memtime();

@@ -19,8 +19,6 @@
 //   lu_trail128_kernel     U12 = L11^-1 A12 (MFMA prologue) and A22 -= L21 U12 at rank 128 on fp32
 //                          MFMA (v_mfma_f32_32x32x2f32): 128-column strips streamed in 64-row
 //                          steps, A22 read + written once per 128 columns.
-// IADMM_LU_RANK128=0 selects the r02 flow (64-column blocks, rank-64 lu_trail_kernel, substitution
-// TRSM) for A/B runs.
 // lu_solve_kernel: one workgroup per instance; P b, then blocked forward (unit L) and backward
 // (U) substitution: 64-row blocks, prefix dot products over coalesced row segments, the 64x64
 // diagonal block solved inside one wave.
@@ -1101,11 +1099,245 @@ __global__ __launch_bounds__(kT2Threads, 1) void lu_trail128_kernel(int N, int P
   }
 }
 
+// Wave-specialised form of lu_trail128_kernel (r04), same arithmetic bit for bit.  The r03 kernel
+// ran every wave through "loads, MFMAs, barrier, output": the memory and MFMA phases of one 8-wave
+// workgroup (the only one on its CU: 143 KB of LDS) overlapped only partly, ~14.6 k cycles per
+// 64-row step against 8.2 k of MFMA issue per SIMD.  Here waves 0-3 (one per SIMD) only compute
+// and waves 4-7 only move data, with one barrier per step:
+//   MFMA wave w, interval t:    columns [32w, 32w + 32) of step t, both 32-row halves (two
+//                               accumulators, U12 operand in registers as before, -L21 from
+//                               Ls[t & 1]), the product -> Cb[t & 1];
+//   memory waves, interval t:   issue the loads of A22 (t) and L21 (t + 1); the output of step t - 1
+//                               (A22 (t - 1), loaded during interval t - 1, minus Cb[(t - 1) & 1]);
+//                               L21 (t + 1) -> Ls[(t + 1) & 1];
+//   barrier.
+// The MFMA waves issue no global access and no VALU beyond their fragment reads; everything the
+// memory waves wait for was issued one interval (one step of MFMAs) earlier.  Per tile the MFMA
+// chain, the product and out = A22 - product are those of lu_trail128_kernel, so the factors are
+// bitwise the same.  (VEC path only: N % 4 == 0 and 16-B aligned rows.)
+// DIAG (tools/lubench128.hip only): 1 = no MFMAs, 2 = no global A22 / L21 traffic in the main loop.
+template <int DIAG = 0>
+__global__ __launch_bounds__(kT2Threads, 1) void lu_trail128ws_kernel(int N, int P, int ntc, float* A,
+                                                                      const float* Linv, const int* perm) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  float* Ls0 = sm;
+  float* Cb0 = sm + 2 * kT2S * kT2K;
+  float* Ut = Ls0;
+  float* Li = Cb0;
+  int* bsrc = reinterpret_cast<int*>(Cb0 + 2 * kT2S * kT2CS);
+  int* tdst = bsrc + kPermMax;
+  int* tsrc = tdst + kPermMax;
+  int* ddst = tsrc + kPermMax;
+  int* dsrc = ddst + kPermMax;
+  unsigned* dbits = reinterpret_cast<unsigned*>(dsrc + kPermMax);
+  const int nwg = gridDim.x, bid = blockIdx.x;
+  const int xcd = bid & 7, local = bid >> 3, q8 = nwg >> 3, r8 = nwg & 7;
+  const int logical = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + local;
+  const size_t b = (size_t)(logical / ntc);
+  const int tc = logical % ntc;
+  float* Ab = A + b * (size_t)N * N;
+  const int c0 = P + kOB, cb = c0 + tc * kT2C;
+  const int nsteps = (N - c0 + kT2S - 1) / kT2S;
+  const int tid = threadIdx.x, lane = tid & 63, il = lane & 31, h = lane >> 5;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  constexpr int NT = kT2Threads;
+
+  // ---- the permutation (as lu_trail128_kernel)
+  const int ndisp = perm ? perm[b * kPermInts + 4 * kPermMax] - kOB : 0;
+  {
+    const int* pb = perm + b * kPermInts;
+    if (tid < kOB) bsrc[tid] = perm ? pb[2 * kPermMax + tid] : P + tid;
+    if (tid < ndisp) { tdst[tid] = pb[kOB + tid]; tsrc[tid] = pb[2 * kPermMax + kOB + tid]; }
+    for (int w = tid; w < 2 * nsteps + 2; w += NT) dbits[w] = 0u;
+  }
+  __syncthreads();
+  if (tid < ndisp) {
+    const int d = tdst[tid];
+    int rank = 0;
+    for (int j = 0; j < ndisp; ++j) rank += tdst[j] < d;
+    ddst[rank] = d;
+    dsrc[rank] = tsrc[tid];
+    atomicOr(&dbits[(d - c0) >> 5], 1u << ((d - c0) & 31));
+  }
+  auto src_row = [&](int row, int ro, unsigned long long m) -> int {
+    if (!((m >> ro) & 1ull)) return row;
+    int lo = 0, hi = ndisp - 1;
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      if (ddst[mid] < row) lo = mid + 1; else hi = mid;
+    }
+    return dsrc[lo];
+  };
+
+  // ---- prologue: U12 = L11^-1 A12 on this strip (all eight waves, as lu_trail128_kernel)
+  constexpr int CPR = kT2C / 4, LPR = kOB / 4;
+#pragma unroll
+  for (int q = 0; q < kOB * kT2C / 4 / NT; ++q) {
+    const int e = tid + NT * q, k = e / CPR, cl = (e % CPR) * 4, col = cb + cl;
+    const float4 x = *reinterpret_cast<const float4*>(Ab + (size_t)bsrc[k] * N + min(col, N - 4));
+    const float4 u = col < N ? x : make_float4(0.f, 0.f, 0.f, 0.f);
+    Ut[(cl + 0) * kT2K + k] = u.x; Ut[(cl + 1) * kT2K + k] = u.y;
+    Ut[(cl + 2) * kT2K + k] = u.z; Ut[(cl + 3) * kT2K + k] = u.w;
+  }
+  const float* Lb = Linv + b * (size_t)kLinvFloats;
+#pragma unroll
+  for (int q = 0; q < kOB * kOB / 4 / NT; ++q) {
+    const int e = tid + NT * q, i = e / (kOB / 4), kk = (e % (kOB / 4)) * 4;
+    *reinterpret_cast<float4*>(Li + i * kT2K + kk) = *reinterpret_cast<const float4*>(Lb + (size_t)i * kOB + kk);
+  }
+  __syncthreads();
+  {
+    const int ti = wave >> 1, tj0 = 2 * (wave & 1);
+    floatx16 u0, u1;
+#pragma unroll
+    for (int v = 0; v < 16; ++v) { u0[v] = 0.f; u1[v] = 0.f; }
+#pragma unroll 4
+    for (int sg = 0; sg < kOB / 8; ++sg) {
+      const float4 fa = *reinterpret_cast<const float4*>(Li + (ti * 32 + il) * kT2K + (kOB / 2) * h + 4 * sg);
+      const float4 f0 = *reinterpret_cast<const float4*>(Ut + (tj0 * 32 + il) * kT2K + (kOB / 2) * h + 4 * sg);
+      const float4 f1 = *reinterpret_cast<const float4*>(Ut + (tj0 * 32 + 32 + il) * kT2K + (kOB / 2) * h + 4 * sg);
+#pragma unroll
+      for (int s4 = 0; s4 < 4; ++s4) {
+        u0 = __builtin_amdgcn_mfma_f32_32x32x2f32(get4(fa, s4), get4(f0, s4), u0, 0, 0, 0);
+        u1 = __builtin_amdgcn_mfma_f32_32x32x2f32(get4(fa, s4), get4(f1, s4), u1, 0, 0, 0);
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int v = 0; v < 16; ++v) {
+      const int i = ti * 32 + 8 * (v >> 2) + 4 * h + (v & 3);
+      Ut[(tj0 * 32 + il) * kT2K + i] = u0[v];
+      Ut[(tj0 * 32 + 32 + il) * kT2K + i] = u1[v];
+    }
+  }
+  __syncthreads();
+  const bool mfma_wave = wave < 4;
+  const int wc = (wave & 3) * 32;
+  float4 ub[kOB / 8];  // MFMA waves: U12[64h + 4sg + 0..3][wc + il] for every step
+  if (mfma_wave) {
+#pragma unroll
+    for (int sg = 0; sg < kOB / 8; ++sg)
+      ub[sg] = *reinterpret_cast<const float4*>(Ut + (wc + il) * kT2K + (kOB / 2) * h + 4 * sg);
+  }
+  __syncthreads();  // Ut consumed: Ls from here on
+
+  // ---- memory waves: 256 threads, 8 float4 of A22 and of L21 per thread and step
+  constexpr int MQ = kT2S * kT2C / 4 / 256;
+  const int mt = tid - 256;
+  auto loadC = [&](int step, float4 (&c)[MQ]) {
+    const unsigned long long m = *reinterpret_cast<const unsigned long long*>(dbits + 2 * step);
+#pragma unroll
+    for (int q = 0; q < MQ; ++q) {
+      const int e = mt + 256 * q, ro = e / CPR, row = c0 + step * kT2S + ro, col = cb + (e % CPR) * 4;
+      c[q] = *reinterpret_cast<const float4*>(Ab + (size_t)min(src_row(row, ro, m), N - 1) * N + min(col, N - 4));
+    }
+  };
+  auto loadL = [&](int step, float4 (&l)[MQ]) {
+#pragma unroll
+    for (int q = 0; q < MQ; ++q) {
+      const int e = mt + 256 * q, row = c0 + step * kT2S + e / LPR;
+      l[q] = *reinterpret_cast<const float4*>(Ab + (size_t)min(row, N - 1) * N + P + (e % LPR) * 4);
+    }
+  };
+  auto writeL = [&](int step, const float4 (&l)[MQ]) {
+    float* Ls = Ls0 + (step & 1) * (kT2S * kT2K);
+#pragma unroll
+    for (int q = 0; q < MQ; ++q) {
+      const int e = mt + 256 * q;
+      *reinterpret_cast<float4*>(Ls + (e / LPR) * kT2K + (e % LPR) * 4) = l[q];
+    }
+  };
+  auto storeOut = [&](int step, float4 (&c)[MQ]) {
+    const float* Cb = Cb0 + (step & 1) * (kT2S * kT2CS);
+#pragma unroll
+    for (int q = 0; q < MQ; ++q) {
+      const int e = mt + 256 * q, row = c0 + step * kT2S + e / CPR, col = cb + (e % CPR) * 4;
+      const float4 pr = *reinterpret_cast<const float4*>(Cb + (e / CPR) * kT2CS + (e % CPR) * 4);
+      c[q].x -= pr.x; c[q].y -= pr.y; c[q].z -= pr.z; c[q].w -= pr.w;
+      if (row < N && col < N) *reinterpret_cast<float4*>(Ab + (size_t)row * N + col) = c[q];
+    }
+  };
+  // ---- MFMA waves: product of step t -> Cb[t & 1]
+  auto product = [&](int step) {
+    const float* Ls = Ls0 + (step & 1) * (kT2S * kT2K);
+    float* Cb = Cb0 + (step & 1) * (kT2S * kT2CS);
+    floatx16 a0, a1;
+#pragma unroll
+    for (int v = 0; v < 16; ++v) { a0[v] = 0.f; a1[v] = 0.f; }
+    if constexpr (DIAG != 1) {
+#pragma unroll
+      for (int sg = 0; sg < kOB / 8; ++sg) {
+        const float4 f0 = *reinterpret_cast<const float4*>(Ls + il * kT2K + (kOB / 2) * h + 4 * sg);
+        const float4 f1 = *reinterpret_cast<const float4*>(Ls + (32 + il) * kT2K + (kOB / 2) * h + 4 * sg);
+#pragma unroll
+        for (int s4 = 0; s4 < 4; ++s4) {
+          a0 = __builtin_amdgcn_mfma_f32_32x32x2f32(get4(f0, s4), get4(ub[sg], s4), a0, 0, 0, 0);
+          a1 = __builtin_amdgcn_mfma_f32_32x32x2f32(get4(f1, s4), get4(ub[sg], s4), a1, 0, 0, 0);
+        }
+      }
+    }
+#pragma unroll
+    for (int v = 0; v < 16; ++v) {
+      const int r = 8 * (v >> 2) + 4 * h + (v & 3);
+      Cb[r * kT2CS + wc + il] = a0[v];
+      Cb[(32 + r) * kT2CS + wc + il] = a1[v];
+    }
+  };
+
+  if (mfma_wave) {
+    __syncthreads();  // Ls[0] = L21 (0)
+    for (int step = 0; step < nsteps; ++step) {
+      product(step);
+      __syncthreads();
+    }
+    __syncthreads();  // the memory waves' drain interval
+  } else {
+    float4 ca[MQ], cbk[MQ], l[MQ];
+    if (DIAG != 2) loadL(0, l);
+    writeL(0, l);
+    __syncthreads();
+    // interval t: loads of A22 (t) and L21 (t + 1); output of step t - 1; L21 (t + 1) -> Ls.
+    // Unrolled by two so the A22 register sets are static (cur = A22 (t), prv = A22 (t - 1)).
+    auto interval = [&](int step, float4 (&cur)[MQ], float4 (&prv)[MQ], bool out) {
+      if (DIAG != 2) {
+        loadC(step, cur);
+        loadL(step + 1, l);
+      }
+      if (out && DIAG != 2) storeOut(step - 1, prv);
+      writeL(step + 1, l);
+      __syncthreads();
+    };
+    interval(0, ca, cbk, false);
+    int step = 1;
+    for (; step + 1 < nsteps; step += 2) {
+      interval(step, cbk, ca, true);
+      interval(step + 1, ca, cbk, true);
+    }
+    if (step < nsteps) {
+      interval(step, cbk, ca, true);
+      ++step;
+      if (DIAG != 2) storeOut(step - 1, cbk);
+    } else {
+      if (DIAG != 2) storeOut(step - 1, ca);
+    }
+    __syncthreads();  // (pairs with the MFMA waves' drain barrier)
+  }
+  __syncthreads();  // every gathered load of a block row has completed: U12 to the block rows
+  if (mfma_wave && cb + wc + il < N) {
+#pragma unroll
+    for (int sg = 0; sg < kOB / 8; ++sg) {
+      const int i = (kOB / 2) * h + 4 * sg;
+      float* dst = Ab + (size_t)(P + i) * N + cb + wc + il;
+      dst[0] = ub[sg].x;
+      dst[(size_t)N] = ub[sg].y;
+      dst[2 * (size_t)N] = ub[sg].z;
+      dst[3 * (size_t)N] = ub[sg].w;
+    }
+  }
+}
+
 // Solve (P^T L U) x = b in place for one instance per workgroup.
 constexpr int kDS = kSolveBlk + 1;  // LDS stride of the staged diagonal block
-#ifndef IADMM_SOLVE_LAZY_PIV
-#define IADMM_SOLVE_LAZY_PIV 1
-#endif
 // VEC (N % 4 == 0, 16-B aligned factors): block bounds are multiples of 4, rows 16-B aligned.
 // NT threads per workgroup: 256 (4 workgroups per CU) when the batch fills the CUs four times
 // over, 512 / 1024 for smaller batches (config 4's 256-instance chunks: one workgroup per CU, so
@@ -1123,17 +1355,6 @@ __global__ __launch_bounds__(NT, NT == 256 ? 4 : (NT == 512 ? 2 : 1)) void lu_so
   float* xb = X + b * N;
 #pragma unroll 8
   for (int i = tid; i < N; i += NT) x[i] = xb[i];
-  __syncthreads();
-  if (!IADMM_SOLVE_LAZY_PIV && wave == 0) {  // all interchanges up front, 64 pivots per load
-    for (int i0 = 0; i0 < N; i0 += 64) {
-      const int pv = piv[b * N + min(i0 + lane, N - 1)] - 1;
-      const int n = min(64, N - i0);
-      for (int j = 0; j < n; ++j) {
-        const int p = __shfl(pv, j, 64);
-        if (lane == 0 && p != i0 + j) { const float t = x[i0 + j]; x[i0 + j] = x[p]; x[p] = t; }
-      }
-    }
-  }
   __syncthreads();
   // The row interchanges (P b) are applied lazily, block by block: interchange i touches positions i
   // and piv[i] - 1 >= i only, so positions below k0 are final once those of rows < k0 are done.  Wave 0
@@ -1162,7 +1383,7 @@ __global__ __launch_bounds__(NT, NT == 256 ? 4 : (NT == 512 ? 2 : 1)) void lu_so
           D[(idx / kSolveBlk) * kDS + idx % kSolveBlk] = dreg[q];
         }
       }
-      if (IADMM_SOLVE_LAZY_PIV && pass == 0 && wave == 0) {
+      if (pass == 0 && wave == 0) {
         const int pv = piv[b * N + k0 + min(lane, nbk - 1)] - 1;
         for (int j = 0; j < nbk; ++j) {
           const int p = __shfl(pv, j, 64);
@@ -1340,10 +1561,6 @@ static int lu_rank64(int64_t B, int64_t N, int K0, int cend, int cmax, float* A,
   return 0;
 }
 
-#ifndef IADMM_LU_RANK128
-#define IADMM_LU_RANK128 1   // 0: the r02 flow (rank-64 trailing update per 64 columns; tools A/B only)
-#endif
-
 static int lu_factor_blocks(int64_t B, int64_t N, float* A, int* piv, int* info, int* perm, float* linv,
                             hipStream_t s) {
   const bool vec = (N % 4 == 0) && aligned16(A);
@@ -1353,15 +1570,6 @@ static int lu_factor_blocks(int64_t B, int64_t N, float* A, int* piv, int* info,
   IADMM_ALLOW_LDS(lu_trail128_kernel<true>, kT2Lds);
   IADMM_ALLOW_LDS(lu_trail128_kernel<false>, kT2Lds);
   int rc = 0;
-  if (!IADMM_LU_RANK128) {
-    for (int K0 = 0; K0 < N && !rc; K0 += kBlk) {
-      const int cend = (int)std::min<int64_t>(N, K0 + kBlk);
-      rc = lu_factor_half(B, N, K0, cend, A, piv, info, s);
-      if (!rc) rc = lu_swap(B, N, K0, cend, 0, K0, cend, (int)N, (int)N, A, piv, perm, s);
-      if (!rc) rc = lu_rank64(B, N, K0, cend, (int)N, A, vec, s);
-    }
-    return rc;
-  }
   for (int P = 0; P < N && !rc; P += kOB) {
     const int n_ = (int)N;
     const int c1 = std::min(n_, P + kBlk), c2 = std::min(n_, P + kOB);

@@ -1,0 +1,78 @@
+// Box-ceiling probes: the fp32 MFMA rate and the HBM copy rate THIS box
+// delivers, measured in-process before the bench's timed steps, so a headline fraction can be
+// read against the box as well as against the spec (MI355X boxes differ by a few % in clock and
+// HBM).  Not on the solve path.
+//
+//   probe_mfma_kernel  every wave streams v_mfma_f32_32x32x2_f32 on 8 independent accumulators
+//                      from registers (no memory in the loop): 4096 flop per MFMA per wave; two
+//                      4-wave workgroups per CU = 2 waves per SIMD, the cell kernel's residency.
+//   probe_copy_kernel  grid-stride float4 copy (16-B loads / stores, 8 in flight per thread).
+#include <algorithm>
+
+#include "common.h"
+
+namespace iadmm {
+
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+
+__global__ __launch_bounds__(256, 2) void probe_mfma_kernel(int iters, float* out) {
+  const int tid = threadIdx.x, lane = tid & 63;
+  const float a = 1e-3f * (float)(lane + 1), b = 2e-3f * (float)(lane + 3);
+  floatx16 acc[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j)
+#pragma unroll
+    for (int q = 0; q < 16; ++q) acc[j][q] = 0.f;
+  for (int it = 0; it < iters; ++it) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, acc[j], 0, 0, 0);
+  }
+  float s = 0.f;
+#pragma unroll
+  for (int j = 0; j < 8; ++j)
+#pragma unroll
+    for (int q = 0; q < 16; ++q) s += acc[j][q];
+  out[(size_t)blockIdx.x * blockDim.x + tid] = s;
+}
+
+__global__ __launch_bounds__(256) void probe_copy_kernel(int64_t n4, const float4* __restrict__ src,
+                                                         float4* __restrict__ dst) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  for (; i + 7 * stride < n4; i += 8 * stride) {
+    float4 v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = src[i + u * stride];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) dst[i + u * stride] = v[u];
+  }
+  for (; i < n4; i += stride) dst[i] = src[i];
+}
+
+}  // namespace iadmm
+
+using namespace iadmm;
+
+extern "C" int64_t iadmm_probe_mfma_flop(int64_t blocks, int64_t iters) {
+  return blocks * 4 * iters * 8 * 4096;  // waves x MFMAs per wave x 32*32*2*2
+}
+
+extern "C" int iadmm_probe_mfma(int64_t blocks, int64_t iters, float* out, void* stream) {
+  if (blocks <= 0 || iters <= 0 || iters > 0x7fffffff || blocks > 0x7fffffff || !out) return IADMM_E_ARG;
+  hipLaunchKernelGGL(probe_mfma_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, (int)iters, out);
+  return (int)hipGetLastError();
+}
+
+extern "C" int iadmm_probe_copy(int64_t bytes, const void* src, void* dst, void* stream) {
+  if (bytes <= 0 || !src || !dst) return IADMM_E_ARG;
+  if ((bytes & 15) || (reinterpret_cast<uintptr_t>(src) & 15) || (reinterpret_cast<uintptr_t>(dst) & 15))
+    return IADMM_E_ALIGN;
+  const int64_t n4 = bytes / 16;
+  int dev = 0, cus = 256;
+  (void)hipGetDevice(&dev);
+  (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  const int64_t blocks = std::min<int64_t>((n4 + 255) / 256, (int64_t)cus * 8);
+  hipLaunchKernelGGL(probe_copy_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, n4,
+                     static_cast<const float4*>(src), static_cast<float4*>(dst));
+  return (int)hipGetLastError();
+}

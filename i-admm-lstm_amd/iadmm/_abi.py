@@ -63,6 +63,9 @@ SIGNATURES = {
     "iadmm_kkt_bwd_split": (cint, [i64, i64, i64, i64, vp, vp, vp, vp, vp, vp, f32, vp, vp, vp, vp, vp, vp, vp, i64,
                                    vp]),
     "iadmm_loss_grad_split": (cint, [i64, i64, i64] + [vp] * 14 + [i64, vp]),
+    "iadmm_probe_mfma_flop": (i64, [i64, i64]),
+    "iadmm_probe_mfma": (cint, [i64, i64, vp, vp]),
+    "iadmm_probe_copy": (cint, [i64, vp, vp, vp]),
 }
 
 ERRORS = {-1: "bad argument", -2: "size beyond kernel limit", -3: "misaligned pointer"}

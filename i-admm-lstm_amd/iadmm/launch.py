@@ -58,13 +58,20 @@ def relaunch(script, argv, gpus):
     print(f"[launch] starting {gpus} ranks: {' '.join(cmd[1:])}", file=sys.stderr, flush=True)
     child = subprocess.Popen(cmd, env=dict(os.environ))
 
-    def forward(signum, _frame):  # a timeout's SIGTERM reaches the ranks through the launcher
+    sent = []
+
+    def forward(signum, _frame):  # a `kill <pid>` SIGTERM reaches the ranks through the launcher, once
+        if sent:
+            return
+        sent.append(signum)
         try:
             child.send_signal(signum)
         except ProcessLookupError:
             pass
 
-    for s in (signal.SIGTERM, signal.SIGINT):
-        signal.signal(s, forward)
+    signal.signal(signal.SIGTERM, forward)
+    # Ctrl-C reaches the child directly (same process group); forwarding it as well would give
+    # torch.distributed.run a second SIGINT in the middle of its worker cleanup
+    signal.signal(signal.SIGINT, signal.SIG_IGN)
     rc = child.wait()
     sys.exit(rc if rc >= 0 else 128 - rc)

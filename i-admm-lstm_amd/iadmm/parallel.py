@@ -64,3 +64,44 @@ def max_over_ranks(value, dist=None, device="cpu"):
     t = torch.tensor([float(value)], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t)
+
+
+def gather_records(rec, dist=None):
+    """Every rank's ``rec`` (a small JSON-able dict) in rank order, on every rank
+    (all_gather_object; measurement only).  Without a process group: ``[rec]``."""
+    if dist is None or not dist.is_initialized():
+        return [rec]
+    out = [None] * dist.get_world_size()
+    dist.all_gather_object(out, rec)
+    return out
+
+
+def device_record(local_rank):
+    """Which GPU this rank runs on: name, PCI location and UUID of ``cuda:local_rank``, the
+    process's HIP_VISIBLE_DEVICES / ROCR_VISIBLE_DEVICES, and the host name."""
+    import socket
+    rec = {"local_rank": int(local_rank), "host": socket.gethostname()}
+    for k in ("HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        if os.environ.get(k) is not None:
+            rec[k] = os.environ[k]
+    if torch.cuda.is_available():
+        p = torch.cuda.get_device_properties(local_rank)
+        rec["device"] = p.name
+        rec["pci"] = "{:04x}:{:02x}:{:02x}".format(getattr(p, "pci_domain_id", 0), getattr(p, "pci_bus_id", 0),
+                                                   getattr(p, "pci_device_id", 0))
+        rec["uuid"] = str(getattr(p, "uuid", ""))
+        rec["cus"] = int(p.multi_processor_count)
+    else:
+        rec["device"] = "cpu"
+    return rec
+
+
+def check_tiling(records, global_batch):
+    """The gathered instance ranges (``first``, ``count`` per rank record) tile [0, global_batch)
+    in rank order with no gap or overlap."""
+    pos = 0
+    for r in sorted(records, key=lambda r: r["rank"]):
+        if r["first"] != pos or r["count"] < 0:
+            return False
+        pos += r["count"]
+    return pos == global_batch

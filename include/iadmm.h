@@ -312,6 +312,17 @@ int iadmm_loss_grad_split(int64_t B, int64_t n, int64_t m, const float* Q, const
                           const float* cp, const float* cd, float* primal, float* dual, float* dx,
                           float* dy, float* dz, void* ws, int64_t ws_bytes, void* stream);
 
+/* ------------------------------------------------------------------------------------------
+ * Box-ceiling probes (bench.py roofline.box_ceiling; not on the solve path).
+ *   iadmm_probe_mfma: ``blocks`` 256-thread workgroups, each wave issuing ``iters`` x 8
+ *     v_mfma_f32_32x32x2_f32 from registers; iadmm_probe_mfma_flop(blocks, iters) flop in all;
+ *     out[blocks*256] receives per-thread sums (keeps the MFMAs live).
+ *   iadmm_probe_copy: float4 copy of ``bytes`` (multiple of 16, 16-B aligned src/dst): 2*bytes of
+ *     HBM traffic. */
+int64_t iadmm_probe_mfma_flop(int64_t blocks, int64_t iters);
+int iadmm_probe_mfma(int64_t blocks, int64_t iters, float* out, void* stream);
+int iadmm_probe_copy(int64_t bytes, const void* src, void* dst, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

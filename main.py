@@ -308,6 +308,19 @@ def report_stats(d, x, mi, me, dist):
     return out
 
 
+def save_resume_state(path, model, optimizer, epoch, stopper):
+    """The --resume state file: tensors and plain Python scalars only, so that
+    torch.load(weights_only=True) reads it back (EarlyStopping's best_loss becomes an np.float64
+    after its second improvement, utils.py:40, which the weights-only unpickler refuses).  Written
+    to a temporary file and renamed into place, so a run killed mid-write keeps the previous state."""
+    best = stopper.best_loss
+    state = {"model": model.state_dict(), "optimizer": optimizer.state_dict(), "epoch": int(epoch),
+             "best_loss": None if best is None else float(best), "counter": int(stopper.counter)}
+    tmp = path + ".tmp"
+    torch.save(state, tmp)
+    os.replace(tmp, path)
+
+
 def run_train(args):
     """main.py:187-547 (QP): epochs of TBPTT batches + validation + EarlyStopping."""
     from iadmm import parallel, train
@@ -402,8 +415,7 @@ def run_train(args):
             stop = bool(flag.item())
         history.append((loss, val_obj))
         if args.resume and rank == 0:
-            torch.save({"model": model.state_dict(), "optimizer": optimizer.state_dict(), "epoch": epoch,
-                        "best_loss": stopper.best_loss, "counter": stopper.counter}, args.resume)
+            save_resume_state(args.resume, model, optimizer, epoch, stopper)
         if stop:
             break
     if dist is not None:

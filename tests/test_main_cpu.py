@@ -10,7 +10,7 @@ from conftest import PKG
 
 # the reference times Ruiz scaling, the model() calls, the final unscale and Stage II; it does
 # not time the zero-fills of the state (allocated before start_time, main.py:836-841) or metrics
-TIMED = {"scaling", "iterations", "unscale", "stage2_assemble", "stage2_factor", "stage2_iterations"}
+TIMED = {"scaling", "setup", "iterations", "unscale", "stage2_assemble", "stage2_factor", "stage2_iterations"}
 
 
 def _span_names():
@@ -23,7 +23,7 @@ def _span_names():
 
 def test_timed_seconds_sums_only_the_reference_timed_spans():
     names = _span_names()
-    assert {"scaling", "iterations", "unscale", "untimed:setup", "untimed:metrics"} <= names
+    assert {"scaling", "setup", "iterations", "unscale", "untimed:setup", "untimed:metrics"} <= names
     spans = {k: 1000.0 for k in names}
     spans.update({"k:lstm_cell": 5000.0, "hist:metrics": 7000.0})
     counted = {k for k in spans if main.timed_seconds({k: spans[k]}) > 0}
@@ -41,3 +41,27 @@ def test_stage2_chunks_are_balanced():
     assert solver.stage2_chunk(5, 100, budget_bytes=2 * per(100)) == 2
     assert solver.stage2_chunk(7, 100, budget_bytes=3 * per(100)) == 3
     assert solver.stage2_chunk(3, 100, budget_bytes=0) == 1
+
+
+def test_resume_state_reloads_weights_only_after_np_best_loss(tmp_path):
+    """EarlyStopping's best_loss is an np.float64 after its second improvement (utils.py:40, the
+    reference's np.min); the --resume state file must still load with weights_only=True, and the
+    write goes through a temporary file renamed into place."""
+    import numpy as np
+    import torch
+    from utils import EarlyStopping
+    model = torch.nn.Linear(3, 2)
+    opt = torch.optim.Adam(model.parameters(), lr=1e-3)
+    stopper = EarlyStopping(str(tmp_path / "ck.pth"), patience=5)
+    stopper.step(2.0, model, "min", 1.0)
+    stopper.step(1.5, model, "min", 1.0)
+    assert isinstance(stopper.best_loss, np.floating)
+    path = str(tmp_path / "resume.pt")
+    main.save_resume_state(path, model, opt, 3, stopper)
+    assert not os.path.exists(path + ".tmp")
+    st = torch.load(path, weights_only=True)
+    assert st["best_loss"] == 1.5 and type(st["best_loss"]) is float
+    assert st["epoch"] == 3 and st["counter"] == 0
+    stopper.best_loss = None
+    main.save_resume_state(path, model, opt, 4, stopper)
+    assert torch.load(path, weights_only=True)["best_loss"] is None
