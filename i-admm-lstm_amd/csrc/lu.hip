@@ -23,6 +23,13 @@
 // (U) substitution: 64-row blocks, prefix dot products over coalesced row segments, the 64x64
 // diagonal block solved inside one wave.
 //
+// Rounding (r04): every multiply-subtract of the VALU paths (panel rank-1 updates, in-half updates,
+// the in-panel and TRSM substitutions, the solve's diagonal blocks) is one fmaf, a single rounding
+// per term as in LAPACK's ?getf2 / ?trsm / ?gemm on FMA hardware (the library builds with
+// -ffp-contract=off so that the elementwise kernels keep the reference's mul-then-add rounding; the
+// LU has no such reference order, and the r03 two-rounding form measured a 1.3-1.8x larger
+// factorisation backward error than MKL's sgetrf on the KKT matrices: tools/lu_diag.py).
+//
 // Pivots are stored 1-based, LAPACK / torch.linalg.lu_factor convention (row i was swapped with
 // row piv[i]-1), so (LU, piv) also feeds torch.linalg.lu_solve.  info[b] = first i+1 with a zero
 // pivot (0 = non-singular), LAPACK convention.
@@ -131,7 +138,7 @@ IADMM_DEV void panel_finish(float* Ab, int N, int K0, int k0, int nb, int cend, 
     for (int i = 1; i < NB; ++i) {
       float s = x[i];
 #pragma unroll
-      for (int l = 0; l < i; ++l) s = s - L11[i][l] * x[l];
+      for (int l = 0; l < i; ++l) s = fmaf(-L11[i][l], x[l], s);
       x[i] = s;
       // (one row's L11 reads at a time: hoisting all 120 of them would cost the panel kernels
       // their fourth workgroup per CU)
@@ -259,7 +266,7 @@ __global__ __launch_bounds__(NT, NT <= 256 ? (M <= 6 ? 4 : 2) : 1) void lu_panel
 #pragma unroll
             for (int c = 0; c < kNB; ++c) {  // static register indices: j is not a compile-time constant
               if (c == j) a[m][c] = l;
-              else if (c > j) a[m][c] = a[m][c] - l * pr[c];
+              else if (c > j) a[m][c] = fmaf(-l, pr[c], a[m][c]);
             }
           }
         }
@@ -353,7 +360,7 @@ __global__ __launch_bounds__(NT, 1) void lu_panel_global_kernel(int N, int K0, i
         float* row = Ab + (size_t)r * N + k0;
         const float l = row[j] * rcp;
         row[j] = l;
-        for (int cc = j + 1; cc < nb; ++cc) row[cc] = row[cc] - l * prw[cc];
+        for (int cc = j + 1; cc < nb; ++cc) row[cc] = fmaf(-l, prw[cc], row[cc]);
       }
     }
     __syncthreads();  // the next column's search reads the updated panel; prw is rewritten
@@ -416,7 +423,7 @@ __global__ __launch_bounds__(256) void lu_update_block_kernel(int N, int k0, int
     if (idx < kUpdRows * kW && r < rows && c < w) {
       float v = a[q];
 #pragma unroll
-      for (int li = 0; li < NB; ++li) v = v - Ls[r][li] * Us[li][c];
+      for (int li = 0; li < NB; ++li) v = fmaf(-Ls[r][li], Us[li][c], v);
       Ab[(size_t)(r0 + r) * N + c0 + c] = v;
     }
   }
@@ -479,7 +486,7 @@ __global__ __launch_bounds__(256) void lu_update_block_vec_kernel(int N, int k0,
       for (int li = 0; li < NB; ++li) {
         const float lv = Ls[r][li];
         const float4 uv = *reinterpret_cast<const float4*>(&Us[li][c]);
-        v.x = v.x - lv * uv.x; v.y = v.y - lv * uv.y; v.z = v.z - lv * uv.z; v.w = v.w - lv * uv.w;
+        v.x = fmaf(-lv, uv.x, v.x); v.y = fmaf(-lv, uv.y, v.y); v.z = fmaf(-lv, uv.z, v.z); v.w = fmaf(-lv, uv.w, v.w);
       }
       *reinterpret_cast<float4*>(Ab + (size_t)(r0 + r) * N + c0 + c) = v;
     }
@@ -570,7 +577,7 @@ __global__ __launch_bounds__(256) void lu_swap_kernel(int N, int K0, int nbk, in
       for (int i = 1; i < kBlk; ++i) {
         float s = x[i];
 #pragma unroll
-        for (int l = 0; l < i; ++l) s = s - Ld[i][l] * x[l];
+        for (int l = 0; l < i; ++l) s = fmaf(-Ld[i][l], x[l], s);
         x[i] = s;
       }
     }
@@ -1107,9 +1114,9 @@ __global__ __launch_bounds__(kT2Threads, 1) void lu_trail128_kernel(int N, int P
 //   MFMA wave w, interval t:    columns [32w, 32w + 32) of step t, both 32-row halves (two
 //                               accumulators, U12 operand in registers as before, -L21 from
 //                               Ls[t & 1]), the product -> Cb[t & 1];
-//   memory waves, interval t:   issue the loads of A22 (t) and L21 (t + 1); the output of step t - 1
+//   memory waves, interval t:   issue the loads of A22 (t) and L21 (t + 2); the output of step t - 1
 //                               (A22 (t - 1), loaded during interval t - 1, minus Cb[(t - 1) & 1]);
-//                               L21 (t + 1) -> Ls[(t + 1) & 1];
+//                               L21 (t + 1), loaded during interval t - 1, -> Ls[(t + 1) & 1];
 //   barrier.
 // The MFMA waves issue no global access and no VALU beyond their fragment reads; everything the
 // memory waves wait for was issued one interval (one step of MFMAs) earlier.  Per tile the MFMA
@@ -1292,29 +1299,34 @@ __global__ __launch_bounds__(kT2Threads, 1) void lu_trail128ws_kernel(int N, int
     }
     __syncthreads();  // the memory waves' drain interval
   } else {
-    float4 ca[MQ], cbk[MQ], l[MQ];
-    if (DIAG != 2) loadL(0, l);
-    writeL(0, l);
+    // interval t: loads of A22 (t) and L21 (t + 2); output of step t - 1 (A22 loaded in interval
+    // t - 1); L21 (t + 1) (loaded in interval t - 1) -> Ls.  Everything waited for was issued one
+    // interval earlier.  Unrolled by two so the register sets are static.
+    float4 ca[MQ], cbk[MQ], la[MQ], lb[MQ];
+    if (DIAG != 2) {
+      loadL(0, la);
+      loadL(1, lb);
+    }
+    writeL(0, la);
     __syncthreads();
-    // interval t: loads of A22 (t) and L21 (t + 1); output of step t - 1; L21 (t + 1) -> Ls.
-    // Unrolled by two so the A22 register sets are static (cur = A22 (t), prv = A22 (t - 1)).
-    auto interval = [&](int step, float4 (&cur)[MQ], float4 (&prv)[MQ], bool out) {
+    auto interval = [&](int step, float4 (&cur)[MQ], float4 (&prv)[MQ], float4 (&lnew)[MQ], float4 (&lold)[MQ],
+                        bool out) {
       if (DIAG != 2) {
         loadC(step, cur);
-        loadL(step + 1, l);
+        loadL(step + 2, lnew);
       }
       if (out && DIAG != 2) storeOut(step - 1, prv);
-      writeL(step + 1, l);
+      writeL(step + 1, lold);
       __syncthreads();
     };
-    interval(0, ca, cbk, false);
+    interval(0, ca, cbk, la, lb, false);
     int step = 1;
     for (; step + 1 < nsteps; step += 2) {
-      interval(step, cbk, ca, true);
-      interval(step + 1, ca, cbk, true);
+      interval(step, cbk, ca, lb, la, true);
+      interval(step + 1, ca, cbk, la, lb, true);
     }
     if (step < nsteps) {
-      interval(step, cbk, ca, true);
+      interval(step, cbk, ca, lb, la, true);
       ++step;
       if (DIAG != 2) storeOut(step - 1, cbk);
     } else {
@@ -1442,13 +1454,13 @@ __global__ __launch_bounds__(NT, NT == 256 ? 4 : (NT == 512 ? 2 : 1)) void lu_so
         if (pass == 0) {
           for (int j = 0; j < nbk; ++j) {
             const float xj = __shfl(v, j, 64);
-            if (lane > j && lane < nbk) v = v - D[lane * kDS + j] * xj;
+            if (lane > j && lane < nbk) v = fmaf(-D[lane * kDS + j], xj, v);
           }
         } else {
           for (int j = nbk - 1; j >= 0; --j) {
             const float vj = __shfl(v, j, 64) / D[j * kDS + j];
             if (lane == j) v = vj;
-            if (lane < j) v = v - D[lane * kDS + j] * vj;
+            if (lane < j) v = fmaf(-D[lane * kDS + j], vj, v);
           }
         }
         if (lane < nbk) x[k0 + lane] = v;

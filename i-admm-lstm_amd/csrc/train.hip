@@ -121,6 +121,9 @@ struct CellBwdArgs {
 constexpr int kCellBwdLdsVec = kRingFloats * 4;
 constexpr int kCellBwdLdsScalar = (128 + kRows) * kLD * 4;
 
+template <bool VEC, bool K16>
+IADMM_DEV void cell_bwd_tile(const CellBwdArgs& a, int jt, int rt, float* dsm, float* sW, float (*swh)[kJT]);
+
 template <bool VEC, bool K16 = false>
 __global__ __launch_bounds__(256, 2) void lstm_cell_bwd_kernel(CellBwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) float dsm[];
@@ -128,6 +131,11 @@ __global__ __launch_bounds__(256, 2) void lstm_cell_bwd_kernel(CellBwdArgs a) {
   __shared__ float swh[4][kJT];
   int jt, rt;
   cell_tile_of_block(a.njt, jt, rt);
+  cell_bwd_tile<VEC, K16>(a, jt, rt, dsm, sW, swh);
+}
+
+template <bool VEC, bool K16>
+IADMM_DEV void cell_bwd_tile(const CellBwdArgs& a, int jt, int rt, float* dsm, float* sW, float (*swh)[kJT]) {
   const int tid = threadIdx.x, lane = tid & 63, jl = lane & 31, hf = lane >> 5;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int h = a.h;

@@ -6,7 +6,7 @@ src=$1; out=$2
 obj=$(mktemp -d /tmp/var_obj_XXXX)
 FLAGS="-O3 -std=c++17 --offload-arch=gfx950 -fPIC -ffp-contract=off -munsafe-fp-atomics -Wno-unused-result -mllvm -disable-promote-alloca-to-lds ${EXTRA:-}"
 pids=()
-for f in kkt lstm lstm_f16x3 admm ruiz lu gemm train metric_bwd; do
+for f in kkt lstm lstm_f16x3 admm ruiz lu gemm train metric_bwd probe; do
   /opt/rocm/bin/hipcc $FLAGS -c "$src/csrc/$f.hip" -o "$obj/$f.o" &
   pids+=($!)
 done
