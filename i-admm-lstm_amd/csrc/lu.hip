@@ -41,6 +41,12 @@
 namespace iadmm {
 
 typedef float floatx16 __attribute__((ext_vector_type(16)));
+typedef __attribute__((address_space(3))) void lds_void;
+
+template <int N>
+IADMM_DEV void vm_wait() {  // s_waitcnt vmcnt(N), other counters untouched (gfx9 encoding)
+  __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
+}
 
 constexpr int kNB = 16;
 constexpr int kPanelMaxM = 8;      // panel rows per thread: N <= 8 * 256 (12 rows spilled 782 VGPRs)
@@ -1123,8 +1129,10 @@ __global__ __launch_bounds__(kT2Threads, 1) void lu_trail128_kernel(int N, int P
 // chain, the product and out = A22 - product are those of lu_trail128_kernel, so the factors are
 // bitwise the same.  (VEC path only: N % 4 == 0 and 16-B aligned rows.)
 // DIAG (tools/lubench128.hip only): 1 = no MFMAs, 2 = no global A22 / L21 traffic in the main loop.
+constexpr int kWSThreads = 768;  // 4 MFMA waves + 8 memory waves (two per SIMD)
+constexpr int kWSMaxN = 32767;   // the LDS-DMA buffer spans one instance: N * N * 4 < 2^32
 template <int DIAG = 0>
-__global__ __launch_bounds__(kT2Threads, 1) void lu_trail128ws_kernel(int N, int P, int ntc, float* A,
+__global__ __launch_bounds__(kWSThreads, 1) void lu_trail128ws_kernel(int N, int P, int ntc, float* A,
                                                                       const float* Linv, const int* perm) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   float* Ls0 = sm;
@@ -1155,7 +1163,7 @@ __global__ __launch_bounds__(kT2Threads, 1) void lu_trail128ws_kernel(int N, int
     const int* pb = perm + b * kPermInts;
     if (tid < kOB) bsrc[tid] = perm ? pb[2 * kPermMax + tid] : P + tid;
     if (tid < ndisp) { tdst[tid] = pb[kOB + tid]; tsrc[tid] = pb[2 * kPermMax + kOB + tid]; }
-    for (int w = tid; w < 2 * nsteps + 2; w += NT) dbits[w] = 0u;
+    for (int w = tid; w < 2 * nsteps + 2; w += kWSThreads) dbits[w] = 0u;
   }
   __syncthreads();
   if (tid < ndisp) {
@@ -1166,7 +1174,7 @@ __global__ __launch_bounds__(kT2Threads, 1) void lu_trail128ws_kernel(int N, int
     dsrc[rank] = tsrc[tid];
     atomicOr(&dbits[(d - c0) >> 5], 1u << ((d - c0) & 31));
   }
-  auto src_row = [&](int row, int ro, unsigned long long m) -> int {
+  auto src_row = [&](int row, int ro, unsigned long long m) __attribute__((always_inline)) -> int {
     if (!((m >> ro) & 1ull)) return row;
     int lo = 0, hi = ndisp - 1;
     while (lo < hi) {
@@ -1176,10 +1184,12 @@ __global__ __launch_bounds__(kT2Threads, 1) void lu_trail128ws_kernel(int N, int
     return dsrc[lo];
   };
 
-  // ---- prologue: U12 = L11^-1 A12 on this strip (all eight waves, as lu_trail128_kernel)
+  // ---- prologue: U12 = L11^-1 A12 on this strip (waves 0-7, as lu_trail128_kernel)
   constexpr int CPR = kT2C / 4, LPR = kOB / 4;
+  const bool pro = tid < NT;
 #pragma unroll
   for (int q = 0; q < kOB * kT2C / 4 / NT; ++q) {
+    if (!pro) break;
     const int e = tid + NT * q, k = e / CPR, cl = (e % CPR) * 4, col = cb + cl;
     const float4 x = *reinterpret_cast<const float4*>(Ab + (size_t)bsrc[k] * N + min(col, N - 4));
     const float4 u = col < N ? x : make_float4(0.f, 0.f, 0.f, 0.f);
@@ -1189,11 +1199,13 @@ __global__ __launch_bounds__(kT2Threads, 1) void lu_trail128ws_kernel(int N, int
   const float* Lb = Linv + b * (size_t)kLinvFloats;
 #pragma unroll
   for (int q = 0; q < kOB * kOB / 4 / NT; ++q) {
+    if (!pro) break;
     const int e = tid + NT * q, i = e / (kOB / 4), kk = (e % (kOB / 4)) * 4;
     *reinterpret_cast<float4*>(Li + i * kT2K + kk) = *reinterpret_cast<const float4*>(Lb + (size_t)i * kOB + kk);
   }
   __syncthreads();
-  {
+  floatx16 pu0, pu1;
+  if (pro) {
     const int ti = wave >> 1, tj0 = 2 * (wave & 1);
     floatx16 u0, u1;
 #pragma unroll
@@ -1209,12 +1221,17 @@ __global__ __launch_bounds__(kT2Threads, 1) void lu_trail128ws_kernel(int N, int
         u1 = __builtin_amdgcn_mfma_f32_32x32x2f32(get4(fa, s4), get4(f1, s4), u1, 0, 0, 0);
       }
     }
-    __syncthreads();
+    pu0 = u0;
+    pu1 = u1;
+  }
+  __syncthreads();  // A12^T and L11^-1 consumed
+  if (pro) {
+    const int ti = wave >> 1, tj0 = 2 * (wave & 1);
 #pragma unroll
     for (int v = 0; v < 16; ++v) {
       const int i = ti * 32 + 8 * (v >> 2) + 4 * h + (v & 3);
-      Ut[(tj0 * 32 + il) * kT2K + i] = u0[v];
-      Ut[(tj0 * 32 + 32 + il) * kT2K + i] = u1[v];
+      Ut[(tj0 * 32 + il) * kT2K + i] = pu0[v];
+      Ut[(tj0 * 32 + 32 + il) * kT2K + i] = pu1[v];
     }
   }
   __syncthreads();
@@ -1228,59 +1245,86 @@ __global__ __launch_bounds__(kT2Threads, 1) void lu_trail128ws_kernel(int N, int
   }
   __syncthreads();  // Ut consumed: Ls from here on
 
-  // ---- memory waves: 256 threads, 8 float4 of A22 and of L21 per thread and step
-  constexpr int MQ = kT2S * kT2C / 4 / 256;
-  const int mt = tid - 256;
-  auto loadC = [&](int step, float4 (&c)[MQ]) {
+  // ---- memory waves: 512 threads, 4 float4 of A22 per thread and step; L21 goes HBM/L2 -> LDS by
+  // LDS-DMA (buffer_load_dwordx4 ... lds, no registers): Ls rows are 128 floats, unpadded, their
+  // 16-B chunks XOR-swizzled by (row & 15) on the source address (the DMA image is lane-linear), so
+  // the MFMA waves' fragment ds_read_b128 is conflict-free.  The buffer is based at the instance
+  // (offsets < 2^32: N <= kWSMaxN), rows >= N read as zero through its range check.
+  constexpr int MT = kWSThreads - 256;
+  constexpr int MQ = kT2S * kT2C / 4 / MT;
+  constexpr int kLS = kOB;                       // LDS row stride of the DMA'd -L21 tiles
+  constexpr int LPW = kT2S / 2 / (MT / 64);      // DMA instructions (two rows each) per memory wave
+  const int mt = tid - 256, mw = (tid >> 6) - 4;
+  const __amdgpu_buffer_rsrc_t lrs =
+      __builtin_amdgcn_make_buffer_rsrc(Ab, 0, (int)((unsigned)N * (unsigned)N * 4u), 0x00020000);
+  unsigned loff[LPW];
+#pragma unroll
+  for (int i = 0; i < LPW; ++i) {
+    const int rl = 2 * (mw * LPW + i) + (lane >> 5), c = (lane & 31) ^ (rl & 15);
+    loff[i] = (unsigned)rl * (unsigned)N * 4u + (unsigned)(P + 4 * c) * 4u;
+  }
+  auto issueL = [&](int step) __attribute__((always_inline)) {
+    float* Ls = Ls0 + (step & 1) * (kT2S * kLS);
+    const unsigned so = (unsigned)(c0 + step * kT2S) * (unsigned)N * 4u;
+#pragma unroll
+    for (int i = 0; i < LPW; ++i)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(lrs, (lds_void*)(Ls + 2 * (mw * LPW + i) * kLS), 16, loff[i], so, 0, 0);
+  };
+  auto loadC = [&](int step, float4 (&c)[MQ]) __attribute__((always_inline)) {
     const unsigned long long m = *reinterpret_cast<const unsigned long long*>(dbits + 2 * step);
+    // the source rows first (the binary search is a divergent loop), then every load at once
+    int src[MQ];
 #pragma unroll
     for (int q = 0; q < MQ; ++q) {
-      const int e = mt + 256 * q, ro = e / CPR, row = c0 + step * kT2S + ro, col = cb + (e % CPR) * 4;
-      c[q] = *reinterpret_cast<const float4*>(Ab + (size_t)min(src_row(row, ro, m), N - 1) * N + min(col, N - 4));
+      const int e = mt + MT * q, ro = e / CPR, row = c0 + step * kT2S + ro;
+      src[q] = min(src_row(row, ro, m), N - 1);
     }
-  };
-  auto loadL = [&](int step, float4 (&l)[MQ]) {
+    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int q = 0; q < MQ; ++q) {
-      const int e = mt + 256 * q, row = c0 + step * kT2S + e / LPR;
-      l[q] = *reinterpret_cast<const float4*>(Ab + (size_t)min(row, N - 1) * N + P + (e % LPR) * 4);
+      const int e = mt + MT * q, col = cb + (e % CPR) * 4;
+      c[q] = *reinterpret_cast<const float4*>(Ab + (size_t)src[q] * N + min(col, N - 4));
     }
   };
-  auto writeL = [&](int step, const float4 (&l)[MQ]) {
-    float* Ls = Ls0 + (step & 1) * (kT2S * kT2K);
-#pragma unroll
-    for (int q = 0; q < MQ; ++q) {
-      const int e = mt + 256 * q;
-      *reinterpret_cast<float4*>(Ls + (e / LPR) * kT2K + (e % LPR) * 4) = l[q];
-    }
-  };
-  auto storeOut = [&](int step, float4 (&c)[MQ]) {
+  auto storeOut = [&](int step, float4 (&c)[MQ]) __attribute__((always_inline)) {
     const float* Cb = Cb0 + (step & 1) * (kT2S * kT2CS);
 #pragma unroll
     for (int q = 0; q < MQ; ++q) {
-      const int e = mt + 256 * q, row = c0 + step * kT2S + e / CPR, col = cb + (e % CPR) * 4;
+      const int e = mt + MT * q, row = c0 + step * kT2S + e / CPR, col = cb + (e % CPR) * 4;
       const float4 pr = *reinterpret_cast<const float4*>(Cb + (e / CPR) * kT2CS + (e % CPR) * 4);
       c[q].x -= pr.x; c[q].y -= pr.y; c[q].z -= pr.z; c[q].w -= pr.w;
       if (row < N && col < N) *reinterpret_cast<float4*>(Ab + (size_t)row * N + col) = c[q];
     }
   };
   // ---- MFMA waves: product of step t -> Cb[t & 1]
-  auto product = [&](int step) {
-    const float* Ls = Ls0 + (step & 1) * (kT2S * kT2K);
+  const int sw = il & 15;
+  auto product = [&](int step) __attribute__((always_inline)) {
+    const float* Ls = Ls0 + (step & 1) * (kT2S * kLS);
     float* Cb = Cb0 + (step & 1) * (kT2S * kT2CS);
     floatx16 a0, a1;
 #pragma unroll
     for (int v = 0; v < 16; ++v) { a0[v] = 0.f; a1[v] = 0.f; }
     if constexpr (DIAG != 1) {
+      // logical 16-B chunk 16h + sg of rows il and 32 + il sits at chunk 16h + (sg ^ (il & 15));
+      // fragments double-buffered by hand (one MFMA wave per SIMD: nothing else fills a stall)
+      const float* l0 = Ls + il * kLS + (kOB / 2) * h;
+      const float* l1 = l0 + 32 * kLS;
+      float4 f0 = *reinterpret_cast<const float4*>(l0 + 4 * sw), f1 = *reinterpret_cast<const float4*>(l1 + 4 * sw);
 #pragma unroll
       for (int sg = 0; sg < kOB / 8; ++sg) {
-        const float4 f0 = *reinterpret_cast<const float4*>(Ls + il * kT2K + (kOB / 2) * h + 4 * sg);
-        const float4 f1 = *reinterpret_cast<const float4*>(Ls + (32 + il) * kT2K + (kOB / 2) * h + 4 * sg);
+        float4 g0 = f0, g1 = f1;
+        if (sg + 1 < kOB / 8) {
+          g0 = *reinterpret_cast<const float4*>(l0 + 4 * ((sg + 1) ^ sw));
+          g1 = *reinterpret_cast<const float4*>(l1 + 4 * ((sg + 1) ^ sw));
+        }
 #pragma unroll
         for (int s4 = 0; s4 < 4; ++s4) {
           a0 = __builtin_amdgcn_mfma_f32_32x32x2f32(get4(f0, s4), get4(ub[sg], s4), a0, 0, 0, 0);
           a1 = __builtin_amdgcn_mfma_f32_32x32x2f32(get4(f1, s4), get4(ub[sg], s4), a1, 0, 0, 0);
         }
+        __builtin_amdgcn_sched_barrier(0);
+        f0 = g0;
+        f1 = g1;
       }
     }
 #pragma unroll
@@ -1299,34 +1343,32 @@ __global__ __launch_bounds__(kT2Threads, 1) void lu_trail128ws_kernel(int N, int
     }
     __syncthreads();  // the memory waves' drain interval
   } else {
-    // interval t: loads of A22 (t) and L21 (t + 2); output of step t - 1 (A22 loaded in interval
-    // t - 1); L21 (t + 1) (loaded in interval t - 1) -> Ls.  Everything waited for was issued one
-    // interval earlier.  Unrolled by two so the register sets are static.
-    float4 ca[MQ], cbk[MQ], la[MQ], lb[MQ];
-    if (DIAG != 2) {
-      loadL(0, la);
-      loadL(1, lb);
-    }
-    writeL(0, la);
+    // interval t: L21 (t + 1) -> Ls[(t + 1) & 1] (DMA, issued first); the loads of A22 (t); the
+    // output of step t - 1 (A22 loaded in interval t - 1); wait for the DMA; barrier.
+    // Unrolled by two so the A22 register sets are static.
+    float4 ca[MQ], cbk[MQ];
+    if (DIAG != 2) issueL(0);
+    vm_wait<0>();
     __syncthreads();
-    auto interval = [&](int step, float4 (&cur)[MQ], float4 (&prv)[MQ], float4 (&lnew)[MQ], float4 (&lold)[MQ],
-                        bool out) {
+    auto interval = [&](int step, float4 (&cur)[MQ], float4 (&prv)[MQ], bool out) __attribute__((always_inline)) {
       if (DIAG != 2) {
+        issueL(step + 1);
         loadC(step, cur);
-        loadL(step + 2, lnew);
+        if (out) storeOut(step - 1, prv);
       }
-      if (out && DIAG != 2) storeOut(step - 1, prv);
-      writeL(step + 1, lold);
+      __builtin_amdgcn_sched_barrier(0);
+      if (out) vm_wait<2 * MQ>();  // (the DMA, then MQ loads and MQ stores)
+      else vm_wait<MQ>();
       __syncthreads();
     };
-    interval(0, ca, cbk, la, lb, false);
+    interval(0, ca, cbk, false);
     int step = 1;
     for (; step + 1 < nsteps; step += 2) {
-      interval(step, cbk, ca, lb, la, true);
-      interval(step + 1, ca, cbk, la, lb, true);
+      interval(step, cbk, ca, true);
+      interval(step + 1, ca, cbk, true);
     }
     if (step < nsteps) {
-      interval(step, cbk, ca, lb, la, true);
+      interval(step, cbk, ca, true);
       ++step;
       if (DIAG != 2) storeOut(step - 1, cbk);
     } else {
@@ -1580,6 +1622,7 @@ static int lu_factor_blocks(int64_t B, int64_t N, float* A, int* piv, int* info,
   IADMM_ALLOW_LDS((lu_trail_kernel<true, 0, kTC / 2>), kTrailLds);
   IADMM_ALLOW_LDS(lu_trail_kernel<false>, kTrailLds);
   IADMM_ALLOW_LDS(lu_trail128_kernel<true>, kT2Lds);
+  IADMM_ALLOW_LDS(lu_trail128ws_kernel<0>, kT2Lds);
   IADMM_ALLOW_LDS(lu_trail128_kernel<false>, kT2Lds);
   int rc = 0;
   for (int P = 0; P < N && !rc; P += kOB) {
@@ -1605,7 +1648,9 @@ static int lu_factor_blocks(int64_t B, int64_t N, float* A, int* piv, int* info,
     IADMM_CHECK_LAUNCH();
     const int ntc = ((int)N - c2 + kT2C - 1) / kT2C;
     const dim3 grid((unsigned)(B * ntc));
-    if (vec) hipLaunchKernelGGL(lu_trail128_kernel<true>, grid, dim3(kT2Threads), kT2Lds, s, (int)N, P, ntc, A, linv, perm);
+    if (vec && N <= kWSMaxN)
+      hipLaunchKernelGGL(lu_trail128ws_kernel<0>, grid, dim3(kWSThreads), kT2Lds, s, (int)N, P, ntc, A, linv, perm);
+    else if (vec) hipLaunchKernelGGL(lu_trail128_kernel<true>, grid, dim3(kT2Threads), kT2Lds, s, (int)N, P, ntc, A, linv, perm);
     else hipLaunchKernelGGL(lu_trail128_kernel<false>, grid, dim3(kT2Threads), kT2Lds, s, (int)N, P, ntc, A, linv, perm);
     IADMM_CHECK_LAUNCH();
   }

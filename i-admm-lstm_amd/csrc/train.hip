@@ -181,12 +181,15 @@ IADMM_DEV void cell_bwd_tile(const CellBwdArgs& a, int jt, int rt, float* dsm, f
                                  rg = rs(a.g + rbase, nvalid * 4), rdq = rs(a.dq + rbase, nvalid * 4),
                                  rin = rs(a.inpart + ((int64_t)jt * M + rbase) * 2, nvalid * 8);
     const bool full = (jt + 1) * kJT <= h;
-    // Eight steps (r, qq), software-pipelined by one: the loads of step st + 1 are issued before the
-    // stores of step st.  vmcnt counts stores as well as loads and retires them in issue order, so a
-    // load issued after a store cannot be waited for without waiting for that store's write
-    // acknowledgement too: loading at the top of each step (r03 first form) put every step's five
-    // stores (dC, 4 x dP) in front of the next step's loads (rocprof A/B: the stores alone were
-    // 1.2 of 10.4 ms per launch).  sched_barrier(0)s pin that order.
+    // Eight steps (r, qq).  vmcnt counts stores as well as loads and retires them in issue order, so
+    // a load issued after a store cannot be waited for without that store's write acknowledgement
+    // too (r03: with the next step's loads issued before this step's five stores, every step still
+    // waited for the previous step's stores: 1.2 of 10.4 ms per launch).  r04: C, dH', dC' of steps
+    // 0-5 go straight into the idle LDS ring by LDS-DMA before the first store (buffer_load_dwordx4
+    // ... lds; each lane reads back its own 16 B, so no barrier is needed), each wave into its own
+    // 18 KiB (6 steps x 3 operands x 1 KiB: the four waves fill the 72 KiB ring exactly); steps 6
+    // and 7 are register loads issued after step 1, behind only two steps' stores.  The scalars xv,
+    // g, dq of both row blocks are register loads issued with the first batch.
     unsigned vr[2], vo[2], vp[2];
     bool rok[2];
 #pragma unroll
@@ -197,25 +200,28 @@ IADMM_DEV void cell_bwd_tile(const CellBwdArgs& a, int jt, int rt, float* dsm, f
       vo[r] = ((unsigned)row * (unsigned)h + (unsigned)(jt * kJT + 4 * hf)) * 4u;
       vp[r] = ((unsigned)row * (unsigned)(4 * h) + (unsigned)(jt * kJT + 4 * hf)) * 4u;
     }
-    float4 ldv[8][3];
     float rsc[2][3];
+    float4 ldv[2][3];
     auto qa_of = [&](int qq) -> unsigned {
       const bool uok = full || jt * kJT + 8 * qq + 4 * hf < h;
       return uok ? 32u * qq : 0x80000000u;
     };
-    auto issue = [&](int st) {
+    float* ering = dsm + wave * (6 * 3 * 256);  // this wave's slots in the (idle) ring
+    auto dma = [&](int st) __attribute__((always_inline)) {
       const int r = st >> 2, qq = st & 3;
-      if (qq == 0) {
-        rsc[r][0] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rxv, vr[r], 0, 0));
-        rsc[r][1] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rg, vr[r], 0, 0));
-        rsc[r][2] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rdq, vr[r], 0, 0));
-      }
-      const unsigned qa = qa_of(qq);
-      ldv[st][0] = u2f4(__builtin_amdgcn_raw_buffer_load_b128(rC, vo[r] + qa, 0, 0));
-      ldv[st][1] = u2f4(__builtin_amdgcn_raw_buffer_load_b128(rdH, vo[r] + qa, 0, 0));
-      ldv[st][2] = u2f4(__builtin_amdgcn_raw_buffer_load_b128(rdCn, vo[r] + qa, 0, 0));
+      const unsigned o = vo[r] + qa_of(qq);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rC, (lds_void*)(ering + (st * 3 + 0) * 256), 16, o, 0, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rdH, (lds_void*)(ering + (st * 3 + 1) * 256), 16, o, 0, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rdCn, (lds_void*)(ering + (st * 3 + 2) * 256), 16, o, 0, 0, 0);
     };
-    issue(0);
+#pragma unroll
+    for (int st = 0; st < 6; ++st) dma(st);
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+      rsc[r][0] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rxv, vr[r], 0, 0));
+      rsc[r][1] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rg, vr[r], 0, 0));
+      rsc[r][2] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rdq, vr[r], 0, 0));
+    }
     float2v din0 = splat2(0.f), din1 = splat2(0.f);
 #pragma unroll
     for (int st = 0; st < 8; ++st) {
@@ -227,7 +233,19 @@ IADMM_DEV void cell_bwd_tile(const CellBwdArgs& a, int jt, int rt, float* dsm, f
         const int jj0 = 8 * qq + 4 * hf;
         const bool uok = full || jt * kJT + jj0 < h;
         const bool ok4 = rok[r] && uok;
-        const float4 cin4 = ldv[st][0], dh4 = ldv[st][1], dc4 = ldv[st][2];
+        // (the compiler waits for every LDS-DMA before the first read of the ring: one wait per
+        // tile, for the loads only; steps 6 and 7 are register loads it waits for as usual)
+        float4 cin4, dh4, dc4;
+        if (st < 6) {
+          const float4* es = reinterpret_cast<const float4*>(ering + st * 3 * 256) + lane;
+          cin4 = es[0];
+          dh4 = es[64];
+          dc4 = es[128];
+        } else {
+          cin4 = ldv[st - 6][0];
+          dh4 = ldv[st - 6][1];
+          dc4 = ldv[st - 6][2];
+        }
         float4 dC4, dP4[4];
 #pragma unroll
         for (int pp = 0; pp < 2; ++pp) {
@@ -279,8 +297,6 @@ IADMM_DEV void cell_bwd_tile(const CellBwdArgs& a, int jt, int rt, float* dsm, f
           }
         }
         __builtin_amdgcn_sched_barrier(0);
-        if (st + 1 < 8) issue(st + 1);
-        __builtin_amdgcn_sched_barrier(0);
         const unsigned qa = qa_of(qq);
         __builtin_amdgcn_raw_buffer_store_b128(f42u(dC4), rdC, vo[r] + qa, 0, 0);
 #pragma unroll
@@ -294,6 +310,17 @@ IADMM_DEV void cell_bwd_tile(const CellBwdArgs& a, int jt, int rt, float* dsm, f
         const unsigned vi = hf ? 0x80000000u : vr[r] * 2u;
         __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(d0), rin, vi, 0, 0);
         __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(d1), rin, vi + 4u, 0, 0);
+      }
+      if (st == 1) {  // steps 6 and 7 into registers, behind only two steps' stores
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int s6 = 6; s6 < 8; ++s6) {
+          const unsigned o = vo[1] + qa_of(s6 & 3);
+          ldv[s6 - 6][0] = u2f4(__builtin_amdgcn_raw_buffer_load_b128(rC, o, 0, 0));
+          ldv[s6 - 6][1] = u2f4(__builtin_amdgcn_raw_buffer_load_b128(rdH, o, 0, 0));
+          ldv[s6 - 6][2] = u2f4(__builtin_amdgcn_raw_buffer_load_b128(rdCn, o, 0, 0));
+        }
+        __builtin_amdgcn_sched_barrier(0);
       }
     }
   } else {

@@ -20,7 +20,7 @@ __global__ void fill(float* p, int64_t n) {
 template <int WS, int DIAG>
 void launch(int B, int N, int P, float* A, float* Linv) {
   const int ntc = (N - P - kOB + kT2C - 1) / kT2C;
-  if (WS) hipLaunchKernelGGL((lu_trail128ws_kernel<DIAG>), dim3(B * ntc), dim3(kT2Threads), kT2Lds, 0, N, P, ntc, A, Linv, nullptr);
+  if (WS) hipLaunchKernelGGL((lu_trail128ws_kernel<DIAG>), dim3(B * ntc), dim3(kWSThreads), kT2Lds, 0, N, P, ntc, A, Linv, nullptr);
   else hipLaunchKernelGGL((lu_trail128_kernel<true, DIAG>), dim3(B * ntc), dim3(kT2Threads), kT2Lds, 0, N, P, ntc, A, Linv, nullptr);
 }
 
