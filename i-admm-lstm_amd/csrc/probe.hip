@@ -6,7 +6,7 @@
 //   probe_mfma_kernel  every wave streams v_mfma_f32_32x32x2_f32 on 8 independent accumulators
 //                      from registers (no memory in the loop): 4096 flop per MFMA per wave; two
 //                      4-wave workgroups per CU = 2 waves per SIMD, the cell kernel's residency.
-//   probe_copy_kernel  grid-stride float4 copy (16-B loads / stores, 8 in flight per thread).
+//   probe_copy_kernel  float4 copy, one contiguous chunk per workgroup (16-B accesses, 8 in flight per thread).
 #include <algorithm>
 
 #include "common.h"
@@ -37,16 +37,19 @@ __global__ __launch_bounds__(256, 2) void probe_mfma_kernel(int iters, float* ou
 
 __global__ __launch_bounds__(256) void probe_copy_kernel(int64_t n4, const float4* __restrict__ src,
                                                          float4* __restrict__ dst) {
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  for (; i + 7 * stride < n4; i += 8 * stride) {
+  // each workgroup streams one contiguous chunk, 8 x 1 KiB per wave in flight (the KKT sweeps'
+  // access shape; a grid-stride form touching 8 far-apart windows per thread measured 0.56 of spec)
+  const int64_t per = (n4 + gridDim.x - 1) / gridDim.x;
+  const int64_t c0 = (int64_t)blockIdx.x * per, c1 = c0 + per < n4 ? c0 + per : n4;
+  int64_t i = c0 + threadIdx.x;
+  for (; i + 7 * 256 < c1; i += 8 * 256) {
     float4 v[8];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) v[u] = src[i + u * stride];
+    for (int u = 0; u < 8; ++u) v[u] = src[i + u * 256];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) dst[i + u * stride] = v[u];
+    for (int u = 0; u < 8; ++u) dst[i + u * 256] = v[u];
   }
-  for (; i < n4; i += stride) dst[i] = src[i];
+  for (; i < c1; i += 256) dst[i] = src[i];
 }
 
 }  // namespace iadmm

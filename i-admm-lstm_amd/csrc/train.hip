@@ -181,16 +181,17 @@ IADMM_DEV void cell_bwd_tile(const CellBwdArgs& a, int jt, int rt, float* dsm, f
                                  rg = rs(a.g + rbase, nvalid * 4), rdq = rs(a.dq + rbase, nvalid * 4),
                                  rin = rs(a.inpart + ((int64_t)jt * M + rbase) * 2, nvalid * 8);
     const bool full = (jt + 1) * kJT <= h;
-    // Eight steps (r, qq).  vmcnt counts stores as well as loads and retires them in issue order, so
-    // a load issued after a store cannot be waited for without that store's write acknowledgement
-    // too (r03: with the next step's loads issued before this step's five stores, every step still
-    // waited for the previous step's stores: 1.2 of 10.4 ms per launch).  r04: C, dH', dC' of steps
-    // 0-5 go straight into the idle LDS ring by LDS-DMA before the first store (buffer_load_dwordx4
-    // ... lds; each lane reads back its own 16 B, so no barrier is needed), each wave into its own
-    // 18 KiB (6 steps x 3 operands x 1 KiB: the four waves fill the 72 KiB ring exactly); steps 6
-    // and 7 are register loads issued after step 1, behind only two steps' stores.  The scalars xv,
-    // g, dq of both row blocks are register loads issued with the first batch.
-    unsigned vr[2], vo[2], vp[2];
+    // Eight steps (r, qq), software-pipelined by one: the loads of step st + 1 are issued before the
+    // stores of step st (vmcnt counts stores as well as loads and retires them in issue order: a
+    // load issued after a store cannot be waited for alone).
+    // Stores (r04): the accumulator layout gives each store instruction 32 rows x 32 B (lanes jl,
+    // jl + 32 hold units 8qq .. 8qq + 7 of row jl), and such scattered stores are issue-bound at the
+    // texture path -- which the partner workgroup's main loop needs for its LDS-DMA (the r03 "no
+    // stores" build was 1.2 of 10.4 ms faster, although nothing waited for them).  dP (4 of the 5
+    // outputs) is therefore staged per 32-row block in this wave's part of the idle LDS ring,
+    // [gate][row][32 units] with a 36-float row stride (conflict-free 16-B writes), and leaves as 16
+    // stores of 8 rows x 128 B (whole lines); dC stays a direct store per step.
+    unsigned vr[2], vo[2];
     bool rok[2];
 #pragma unroll
     for (int r = 0; r < 2; ++r) {
@@ -198,30 +199,37 @@ IADMM_DEV void cell_bwd_tile(const CellBwdArgs& a, int jt, int rt, float* dsm, f
       rok[r] = row < nvalid;
       vr[r] = (unsigned)row * 4u;
       vo[r] = ((unsigned)row * (unsigned)h + (unsigned)(jt * kJT + 4 * hf)) * 4u;
-      vp[r] = ((unsigned)row * (unsigned)(4 * h) + (unsigned)(jt * kJT + 4 * hf)) * 4u;
     }
+    constexpr int kSR = kJT + 4;                    // staging row stride (floats)
+    static_assert(4 * 4 * kJT * kSR <= kRingFloats, "dP staging must fit in the ring");
+    float* stg = dsm + wave * (4 * kJT * kSR);      // this wave's [4 gates][32 rows][kSR]
+    // transposed dP stores: lane -> row (lane >> 3) + 8 i, 16-B chunk lane & 7 of the gate's 32 units
+    const int trow = lane >> 3, tch = lane & 7;
+    const bool tuok = full || jt * kJT + 4 * tch < h;
+    unsigned tvo[2];
+#pragma unroll
+    for (int r = 0; r < 2; ++r)
+      tvo[r] = tuok ? ((unsigned)(wave * 64 + r * 32 + trow) * (unsigned)(4 * h) + (unsigned)(jt * kJT + 4 * tch)) * 4u
+                    : 0x80000000u;
+    float4 ldv[8][3];
     float rsc[2][3];
-    float4 ldv[2][3];
     auto qa_of = [&](int qq) -> unsigned {
       const bool uok = full || jt * kJT + 8 * qq + 4 * hf < h;
       return uok ? 32u * qq : 0x80000000u;
     };
-    float* ering = dsm + wave * (6 * 3 * 256);  // this wave's slots in the (idle) ring
-    auto dma = [&](int st) __attribute__((always_inline)) {
+    auto issue = [&](int st) {
       const int r = st >> 2, qq = st & 3;
-      const unsigned o = vo[r] + qa_of(qq);
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rC, (lds_void*)(ering + (st * 3 + 0) * 256), 16, o, 0, 0, 0);
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rdH, (lds_void*)(ering + (st * 3 + 1) * 256), 16, o, 0, 0, 0);
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rdCn, (lds_void*)(ering + (st * 3 + 2) * 256), 16, o, 0, 0, 0);
+      if (qq == 0) {
+        rsc[r][0] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rxv, vr[r], 0, 0));
+        rsc[r][1] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rg, vr[r], 0, 0));
+        rsc[r][2] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rdq, vr[r], 0, 0));
+      }
+      const unsigned qa = qa_of(qq);
+      ldv[st][0] = u2f4(__builtin_amdgcn_raw_buffer_load_b128(rC, vo[r] + qa, 0, 0));
+      ldv[st][1] = u2f4(__builtin_amdgcn_raw_buffer_load_b128(rdH, vo[r] + qa, 0, 0));
+      ldv[st][2] = u2f4(__builtin_amdgcn_raw_buffer_load_b128(rdCn, vo[r] + qa, 0, 0));
     };
-#pragma unroll
-    for (int st = 0; st < 6; ++st) dma(st);
-#pragma unroll
-    for (int r = 0; r < 2; ++r) {
-      rsc[r][0] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rxv, vr[r], 0, 0));
-      rsc[r][1] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rg, vr[r], 0, 0));
-      rsc[r][2] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rdq, vr[r], 0, 0));
-    }
+    issue(0);
     float2v din0 = splat2(0.f), din1 = splat2(0.f);
 #pragma unroll
     for (int st = 0; st < 8; ++st) {
@@ -233,19 +241,7 @@ IADMM_DEV void cell_bwd_tile(const CellBwdArgs& a, int jt, int rt, float* dsm, f
         const int jj0 = 8 * qq + 4 * hf;
         const bool uok = full || jt * kJT + jj0 < h;
         const bool ok4 = rok[r] && uok;
-        // (the compiler waits for every LDS-DMA before the first read of the ring: one wait per
-        // tile, for the loads only; steps 6 and 7 are register loads it waits for as usual)
-        float4 cin4, dh4, dc4;
-        if (st < 6) {
-          const float4* es = reinterpret_cast<const float4*>(ering + st * 3 * 256) + lane;
-          cin4 = es[0];
-          dh4 = es[64];
-          dc4 = es[128];
-        } else {
-          cin4 = ldv[st - 6][0];
-          dh4 = ldv[st - 6][1];
-          dc4 = ldv[st - 6][2];
-        }
+        const float4 cin4 = ldv[st][0], dh4 = ldv[st][1], dc4 = ldv[st][2];
         float4 dC4, dP4[4];
 #pragma unroll
         for (int pp = 0; pp < 2; ++pp) {
@@ -297,11 +293,22 @@ IADMM_DEV void cell_bwd_tile(const CellBwdArgs& a, int jt, int rt, float* dsm, f
           }
         }
         __builtin_amdgcn_sched_barrier(0);
+        if (st + 1 < 8) issue(st + 1);
+        __builtin_amdgcn_sched_barrier(0);
         const unsigned qa = qa_of(qq);
         __builtin_amdgcn_raw_buffer_store_b128(f42u(dC4), rdC, vo[r] + qa, 0, 0);
 #pragma unroll
         for (int g = 0; g < 4; ++g)
-          __builtin_amdgcn_raw_buffer_store_b128(f42u(dP4[g]), rdP, vp[r] + (unsigned)(g * h * 4) + qa, 0, 0);
+          *reinterpret_cast<float4*>(stg + (g * kJT + jl) * kSR + jj0) = dP4[g];
+      }
+      if (qq == 3) {  // this row block's dP: 16 stores of 8 rows x 128 B
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const int g = i >> 2, rr = trow + 8 * (i & 3);
+          const float4 v = *reinterpret_cast<const float4*>(stg + (g * kJT + rr) * kSR + 4 * tch);
+          const int so = (8 * (i & 3) * 4 * h + g * h) * 4;
+          __builtin_amdgcn_raw_buffer_store_b128(f42u(v), rdP, tvo[r], so, 0);
+        }
       }
       if (qq == 3) {
         float d0 = din0.x + din0.y, d1 = din1.x + din1.y;
@@ -310,17 +317,6 @@ IADMM_DEV void cell_bwd_tile(const CellBwdArgs& a, int jt, int rt, float* dsm, f
         const unsigned vi = hf ? 0x80000000u : vr[r] * 2u;
         __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(d0), rin, vi, 0, 0);
         __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(d1), rin, vi + 4u, 0, 0);
-      }
-      if (st == 1) {  // steps 6 and 7 into registers, behind only two steps' stores
-        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int s6 = 6; s6 < 8; ++s6) {
-          const unsigned o = vo[1] + qa_of(s6 & 3);
-          ldv[s6 - 6][0] = u2f4(__builtin_amdgcn_raw_buffer_load_b128(rC, o, 0, 0));
-          ldv[s6 - 6][1] = u2f4(__builtin_amdgcn_raw_buffer_load_b128(rdH, o, 0, 0));
-          ldv[s6 - 6][2] = u2f4(__builtin_amdgcn_raw_buffer_load_b128(rdCn, o, 0, 0));
-        }
-        __builtin_amdgcn_sched_barrier(0);
       }
     }
   } else {
