@@ -302,13 +302,23 @@ IADMM_DEV void cell_bwd_tile(const CellBwdArgs& a, int jt, int rt, float* dsm, f
           *reinterpret_cast<float4*>(stg + (g * kJT + jl) * kSR + jj0) = dP4[g];
       }
       if (qq == 3) {  // this row block's dP: 16 stores of 8 rows x 128 B
+        // every value read before the first store (64 VGPRs, free once this block's accumulators
+        // are): an LDS return must not land in the registers of a store still queued for issue
+        // (measured: reading the next value into a just-stored register made dP nondeterministic)
+        float4 tv[16];
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
           const int g = i >> 2, rr = trow + 8 * (i & 3);
-          const float4 v = *reinterpret_cast<const float4*>(stg + (g * kJT + rr) * kSR + 4 * tch);
-          const int so = (8 * (i & 3) * 4 * h + g * h) * 4;
-          __builtin_amdgcn_raw_buffer_store_b128(f42u(v), rdP, tvo[r], so, 0);
+          tv[i] = *reinterpret_cast<const float4*>(stg + (g * kJT + rr) * kSR + 4 * tch);
         }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const int g = i >> 2;
+          const int so = (8 * (i & 3) * 4 * h + g * h) * 4;
+          __builtin_amdgcn_raw_buffer_store_b128(f42u(tv[i]), rdP, tvo[r], so, 0);
+        }
+        __builtin_amdgcn_sched_barrier(0);
       }
       if (qq == 3) {
         float d0 = din0.x + din0.y, d1 = din1.x + din1.y;

@@ -11,3 +11,4 @@ import sys,json
 for l in sys.stdin:
     r=json.loads(l); print(r['lib'].split('/')[-1], round(r['best_ms'],2), [round(x,3) for x in r['solve_ms'][:3]], r['lu_bits_sum'], r['piv_sum'])"
 bash tools/gpu_tests.sh r04h 900 tests/test_train_config5_gpu.py tests/test_train_gpu.py tests/test_cell_gpu.py || exit $?
+timeout -k 10 400 python -u tools/lu_diag.py --N 2000 10000 --batch 2 > gpurun_out/r04h_lu_diag_split.log 2>&1 || exit $?

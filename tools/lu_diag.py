@@ -39,10 +39,18 @@ def unpack(LU, piv):
 def factor_stats(K, LU, piv, ref_piv):
     P, L, U = unpack(LU, piv)
     R = P @ (L @ U) - K
-    out = {"factor_berr": float(R.norm() / K.norm()),
+    N = K.shape[0]
+    # where the residual sits: the U12 rows right of each 128-column block (rows [P, P + 128),
+    # columns >= P + 128: U12 = L11^-1 A12 in the HIP flow), the rest of U, and L
+    ii = torch.arange(N, device=K.device)
+    blk = (ii // 128) * 128
+    u12 = (ii.unsqueeze(1) < N) & (ii.unsqueeze(0) >= (blk + 128).unsqueeze(1))
+    upper = ii.unsqueeze(0) >= ii.unsqueeze(1)
+    parts = {"R_U12": float(R[u12].norm() / K.norm()), "R_Udiag": float(R[upper & ~u12].norm() / K.norm()),
+             "R_L": float(R[~upper].norm() / K.norm())}
+    out = {"factor_berr": float(R.norm() / K.norm()), **parts,
            "factor_berr_max": float(R.abs().max() / K.abs().max()),
            "growth": float(U.abs().max() / K.abs().max())}
-    N = K.shape[0]
     linv = 0.0
     for P0 in range(0, N, 128):
         e = min(N, P0 + 128)
