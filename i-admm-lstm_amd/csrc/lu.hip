@@ -788,20 +788,24 @@ __global__ __launch_bounds__(kTrailThreads, 1) void lu_trail_kernel(int N, int K
 // workgroup reads what it overwrites).
 constexpr int kOB = 2 * kBlk;     // outer block width = rank of the fused trailing update
 constexpr int kT2C = 128;         // trailing update: columns per workgroup strip
-constexpr int kT2S = 64;          //   rows per pipeline step
-constexpr int kT2K = kOB + 4;     //   LDS stride (k) of the U12^T, -L21 and L11^-1 tiles
-constexpr int kT2CS = kT2C + 8;   //   LDS stride of the A22 staging tile
-constexpr int kT2Threads = 512;
+constexpr int kT2S = 32;          //   rows per pipeline step
+constexpr int kT2K = kOB + 4;     //   LDS stride (k) of the U12^T and L21 tiles
+constexpr int kT2CS = kT2C + 8;   //   LDS stride of the product tile
+constexpr int kT2PK = kOB / 2 + 4;  //   LDS stride of the prologue's 64-k half tiles
+constexpr int kT2Threads = 256;   // 4 waves; two workgroups per CU
 // the block's composed row permutation for the gathered loads: the block rows' sources, the displaced
-// rows below the block with their sources (as given, then sorted) and a bitmap of the displaced rows
-constexpr int kT2BitWords = 2 * ((kLuMaxN + kT2S - 1) / kT2S) + 2;
-constexpr int kT2PermInts = 5 * kPermMax + kT2BitWords;
-// -L21 and the product tile double-buffered; the prologue's U12^T over the former, L11^-1 over the latter
-constexpr size_t kT2Lds = (2 * (size_t)kT2S * kT2K + 2 * (size_t)kT2S * kT2CS) * sizeof(float) +
-                          (size_t)kT2PermInts * sizeof(int);
-static_assert(2 * kT2S * kT2K >= kT2C * kT2K, "U12^T staging must fit in the -L21 tiles");
-static_assert(2 * kT2S * kT2CS >= kOB * kT2K, "L11^-1 staging must fit in the product tiles");
-static_assert(kT2Lds <= 160 * 1024, "gfx950 LDS");
+// rows below the block with their sources (as given, then sorted by row), a bitmap of the displaced
+// rows (one word per step) and the rank of each step's first displaced row (one byte per step)
+constexpr int kT2BitWords = (kLuMaxN + kT2S - 1) / kT2S + 2;
+// L21 and the product tile double-buffered; the prologue's half tiles and U12^T over them
+constexpr int kT2MainFloats = 2 * kT2S * kT2K + 2 * kT2S * kT2CS;
+constexpr int kT2ProFloats = 2 * kOB * kT2PK;
+constexpr int kT2AreaFloats = kT2MainFloats > kT2ProFloats ? kT2MainFloats : kT2ProFloats;
+constexpr size_t kT2Lds = (size_t)kT2AreaFloats * sizeof(float) + (size_t)(4 * kPermMax + kT2BitWords) * sizeof(int) +
+                          (size_t)((kT2BitWords + 3) & ~3);
+static_assert(kT2C * kT2K <= kT2AreaFloats, "U12^T staging must fit the area");
+static_assert(kT2C == 128 && kOB == 128, "the wave layout assumes a 128 x 128 block");
+static_assert(2 * kT2Lds <= 160 * 1024, "two workgroups per CU (gfx950 LDS)");
 constexpr int kLinvFloats = kOB * kOB;
 
 // Linv[b] = (unit lower part of A[P:P+128, P:P+128])^-1, row-major 128 x 128.  Thread j computes
@@ -853,39 +857,46 @@ __global__ __launch_bounds__(kOB) void lu_linv_kernel(int N, int P, const float*
 }
 
 // Fused row interchanges, U12 = L11^-1 A12 and A22 -= L21 U12 (rank 128) for the columns right of
-// [P, P + 128).  One workgroup (8 waves, one per CU) per (instance, 128-column strip), all trailing
-// rows.  The block's 128 interchanges (composed by lu_block_perm_kernel: block row P + i takes row
-// pcur[i], each displaced row below the block takes an original block row) get no pass of their
-// own over these columns: the loads gather through the permutation, and the block rows -- the only
-// sources of displaced rows -- are overwritten (with U12) after the last step's loads.
-// (perm == nullptr: no interchanges, tools/lubench128.hip.)
-//   prologue: the gathered A12 (128 x 128, transposed) and L11^-1 into LDS, U12 on MFMA (each wave
-//             two 32 x 32 tiles), transposed into LDS, then each wave's MFMA operand of it -- column
-//             wc + il, k in [64h, 64h + 64): 64 registers -- kept in registers for the whole loop;
-//   main loop: 64-row steps; wave (wr, wc) owns 32 x 32 of a step (v_mfma_f32_32x32x2f32, 64 per
-//             step, -L21 from LDS, U12 from registers).  -L21 and the product tile are
-//             double-buffered in LDS, so a step needs ONE barrier: per wave, step t = issue the
-//             loads of A22 (t + 1) and L21 (t + 2); the MFMAs; product -> Cb[t & 1]; L21 (t + 1)
-//             -> Ls[(t + 1) & 1]; barrier; out = A22 - product for step t (row-contiguous 16-B
-//             global stores, the A22 values already in the registers of the storing thread).  Waves
-//             leave the barrier together but no longer wait for each other's output phase, which
-//             runs beside other waves' MFMAs.
+// [P, P + 128).  One workgroup per (instance, 128-column strip), all trailing rows; 4 waves and 72 KB
+// of LDS, so TWO workgroups share a CU (r04; the r03 form ran one 8-wave workgroup per CU, whose
+// waves all reached their output phase together behind one barrier while the MFMA pipe idled:
+// tools/lubench128.hip, profiles/r04_lubench128_paired.txt).  The block's 128 interchanges
+// (composed by lu_block_perm_kernel: block row P + i takes row pcur[i], each displaced row below the
+// block takes an original block row) get no pass of their own over these columns: the loads gather
+// through the permutation, and the block rows -- the only sources of displaced rows -- are
+// overwritten (with U12) after the last step's loads.  A displaced row finds its source in O(1):
+// sources sorted by row (dsrc), the rank of a step's first displaced row (dpre) plus the popcount
+// of the step's bitmap below the row.  (perm == nullptr: no interchanges, tools/lubench128.hip.)
+//   prologue: U12 = L11^-1 A12 on MFMA in two passes of 64 k (the L11^-1 columns and gathered A12
+//             rows of MFMA k-steps [8p, 8p + 8) of both lane halves; wave w: U12 rows [32w, 32w+32),
+//             four 32 x 32 tiles accumulating across the passes), transposed into LDS, then each
+//             wave's MFMA operand -- column 32w + il, k in [64h, 64h + 64): 64 registers -- kept in
+//             registers for the whole loop;
+//   main loop: 32-row steps; wave w owns columns [32w, 32w + 32) of a step (v_mfma_f32_32x32x2f32,
+//             64 per step, the first on an inline-zero C, L21 fragments read two k-groups ahead,
+//             U12 from registers).  L21 and the product tile are double-buffered in LDS, so a step
+//             needs ONE barrier: per wave, step t = issue the loads of A22 (t + 1) and L21 (t + 2); the
+//             MFMAs; product -> Cb[t & 1]; L21 (t + 1) -> Ls[(t + 1) & 1]; barrier; out = A22 -
+//             product for step t (row-contiguous global stores, the A22 values already in the
+//             registers of the storing thread).
+// Same MFMA chains, products and subtractions as the r03 kernel: bitwise the same factors.
 // Strips of one instance are consecutive logical ids on one XCD (its L2 serves the L21 re-reads).
 // DIAG (tools/lubench128.hip only): 1 = no MFMAs in the main loop, 2 = no global A22 / L21 traffic in it.
 template <bool VEC, int DIAG = 0>
-__global__ __launch_bounds__(kT2Threads, 1) void lu_trail128_kernel(int N, int P, int ntc, float* A,
+__global__ __launch_bounds__(kT2Threads, 2) void lu_trail128_kernel(int N, int P, int ntc, float* A,
                                                                     const float* Linv, const int* perm) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
-  float* Ls0 = sm;                      // 2 x [kT2S rows][kT2K]: -L21 of a step
+  float* Ls0 = sm;                      // 2 x [kT2S rows][kT2K]: L21 of a step
   float* Cb0 = sm + 2 * kT2S * kT2K;    // 2 x [kT2S rows][kT2CS]: product of a step
-  float* Ut = Ls0;                      // prologue: A12^T, then U12^T [kT2C cols][kT2K], over Ls
-  float* Li = Cb0;                      // prologue: L11^-1 [128 rows][kT2K], over Cb
-  int* bsrc = reinterpret_cast<int*>(Cb0 + 2 * kT2S * kT2CS);  // [128] source row of block row P + i
+  float* Lh = sm;                       // prologue pass: its L11^-1 columns [128 rows][kT2PK]
+  float* Uh = sm + kOB * kT2PK;         //                its A12 rows, transposed [128 cols][kT2PK]
+  float* Ut = sm;                       // then U12^T [128 cols][kT2K]
+  int* bsrc = reinterpret_cast<int*>(sm + kT2AreaFloats);  // [128] source row of block row P + i
   int* tdst = bsrc + kPermMax;          // [128] displaced rows and
   int* tsrc = tdst + kPermMax;          // [128] their sources, as given;
-  int* ddst = tsrc + kPermMax;          // [128] the same sorted by row
-  int* dsrc = ddst + kPermMax;          // [128]
-  unsigned* dbits = reinterpret_cast<unsigned*>(dsrc + kPermMax);  // 2 words per step: displaced rows
+  int* dsrc = tsrc + kPermMax;          // [128] the sources sorted by displaced row
+  unsigned* dbits = reinterpret_cast<unsigned*>(dsrc + kPermMax);  // 1 word per step: displaced rows
+  unsigned char* dpre = reinterpret_cast<unsigned char*>(dbits + kT2BitWords);  // rank of a step's first
   const int nwg = gridDim.x, bid = blockIdx.x;
   const int xcd = bid & 7, local = bid >> 3, q8 = nwg >> 3, r8 = nwg & 7;
   const int logical = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + local;
@@ -894,14 +905,15 @@ __global__ __launch_bounds__(kT2Threads, 1) void lu_trail128_kernel(int N, int P
   float* Ab = A + b * (size_t)N * N;
   const int c0 = P + kOB, cb = c0 + tc * kT2C;
   const int nsteps = (N - c0 + kT2S - 1) / kT2S;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, il = lane & 31, h = lane >> 5;
+  const int tid = threadIdx.x, lane = tid & 63, il = lane & 31, h = lane >> 5;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   constexpr int NT = kT2Threads;
 
   typedef typename std::conditional<VEC, float4, float>::type VT;
   constexpr int W = VEC ? 4 : 1;
   constexpr int kCQ = kT2S * kT2C / W / NT;   // A22 accesses per thread per step
-  constexpr int kLQ = kT2S * kOB / W / NT;    // -L21 accesses per thread per step
-  constexpr int kPQ = kOB * kT2C / W / NT;    // A12 / L11^-1 accesses per thread (prologue)
+  constexpr int kLQ = kT2S * kOB / W / NT;    // L21 accesses per thread per step
+  constexpr int kAQ = (kOB / 2) * kT2C / W / NT;  // A12 accesses per thread per prologue pass
   constexpr int CPR = kT2C / W, LPR = kOB / W;
   // main-loop loads: unconditional, from a clamped (valid) address.  Rows >= N / columns >= N only
   // feed products that are never stored, so they need no zero fill -- and a load with no select
@@ -912,20 +924,6 @@ __global__ __launch_bounds__(kT2Threads, 1) void lu_trail128_kernel(int N, int P
     if constexpr (VEC) return *reinterpret_cast<const float4*>(p);
     else return *p;
   };
-  auto ld = [&](int row, int col, bool ok) -> VT {
-    const float* p = Ab + (size_t)row * N + col;
-    if constexpr (VEC) {
-      const float4 x = *reinterpret_cast<const float4*>(p);
-      return ok ? x : make_float4(0.f, 0.f, 0.f, 0.f);
-    } else {
-      const float x = *p;
-      return ok ? x : 0.f;
-    }
-  };
-  auto st_lds = [&](float* d, const VT& v) {
-    if constexpr (VEC) *reinterpret_cast<float4*>(d) = v;
-    else *d = v;
-  };
 
   // ---- the permutation (displaced rows are >= c0 and distinct; <= 128 of them)
   const int ndisp = perm ? perm[b * kPermInts + 4 * kPermMax] - kOB : 0;
@@ -933,88 +931,105 @@ __global__ __launch_bounds__(kT2Threads, 1) void lu_trail128_kernel(int N, int P
     const int* pb = perm + b * kPermInts;
     if (tid < kOB) bsrc[tid] = perm ? pb[2 * kPermMax + tid] : P + tid;
     if (tid < ndisp) { tdst[tid] = pb[kOB + tid]; tsrc[tid] = pb[2 * kPermMax + kOB + tid]; }
-    for (int w = tid; w < 2 * nsteps + 2; w += NT) dbits[w] = 0u;  // (+ the one-past-the-end step)
+    for (int w = tid; w < nsteps + 2; w += NT) { dbits[w] = 0u; dpre[w] = 0; }  // (+ one past the end)
   }
   __syncthreads();
+  int drank = 0, dd = 0;
   if (tid < ndisp) {
-    const int d = tdst[tid];
-    int rank = 0;
-    for (int j = 0; j < ndisp; ++j) rank += tdst[j] < d;
-    ddst[rank] = d;
-    dsrc[rank] = tsrc[tid];
-    atomicOr(&dbits[(d - c0) >> 5], 1u << ((d - c0) & 31));
-  }
-  // (published by the barrier after the prologue's LDS fills below)
-  // source row of trailing row `row` (ro = row - the step's first row; m = that step's bitmap)
-  auto src_row = [&](int row, int ro, unsigned long long m) -> int {
-    if (!((m >> ro) & 1ull)) return row;
-    int lo = 0, hi = ndisp - 1;
-    while (lo < hi) {
-      const int mid = (lo + hi) >> 1;
-      if (ddst[mid] < row) lo = mid + 1; else hi = mid;
-    }
-    return dsrc[lo];
-  };
-
-  // ---- prologue: U12 = L11^-1 A12 on this strip
-#pragma unroll
-  for (int q = 0; q < kPQ; ++q) {  // A12 -> Ut (transposed)
-    const int e = tid + NT * q, k = e / CPR, cl = (e % CPR) * W, col = cb + cl;
-    const VT u = ld(bsrc[k], min(col, N - W), col < N);
-    if constexpr (VEC) {
-      Ut[(cl + 0) * kT2K + k] = u.x; Ut[(cl + 1) * kT2K + k] = u.y;
-      Ut[(cl + 2) * kT2K + k] = u.z; Ut[(cl + 3) * kT2K + k] = u.w;
-    } else {
-      Ut[cl * kT2K + k] = u;
-    }
-  }
-  const float* Lb = Linv + b * (size_t)kLinvFloats;
-#pragma unroll
-  for (int q = 0; q < kOB * kOB / 4 / NT; ++q) {  // L11^-1 -> Li (rows, 16-B pieces)
-    const int e = tid + NT * q, i = e / (kOB / 4), kk = (e % (kOB / 4)) * 4;
-    *reinterpret_cast<float4*>(Li + i * kT2K + kk) = *reinterpret_cast<const float4*>(Lb + (size_t)i * kOB + kk);
+    dd = tdst[tid] - c0;
+    for (int j = 0; j < ndisp; ++j) drank += tdst[j] - c0 < dd;
+    dsrc[drank] = tsrc[tid];
+    atomicOr(&dbits[dd >> 5], 1u << (dd & 31));
   }
   __syncthreads();
-  {
-    const int ti = wave >> 1, tj0 = 2 * (wave & 1);
-    floatx16 u0, u1;
+  if (tid < ndisp && __builtin_popcount(dbits[dd >> 5] & ((1u << (dd & 31)) - 1u)) == 0)
+    dpre[dd >> 5] = (unsigned char)drank;
+  // (published by the prologue's barriers)
+
+  // ---- prologue: U12 = L11^-1 A12 on this strip; wave w: U12 rows [32w, 32w + 32)
+  const float* Lb = Linv + b * (size_t)kLinvFloats;
+  floatx16 u[4];
 #pragma unroll
-    for (int v = 0; v < 16; ++v) { u0[v] = 0.f; u1[v] = 0.f; }
-#pragma unroll 4
-    for (int sg = 0; sg < kOB / 8; ++sg) {
-      const float4 fa = *reinterpret_cast<const float4*>(Li + (ti * 32 + il) * kT2K + (kOB / 2) * h + 4 * sg);
-      const float4 f0 = *reinterpret_cast<const float4*>(Ut + (tj0 * 32 + il) * kT2K + (kOB / 2) * h + 4 * sg);
-      const float4 f1 = *reinterpret_cast<const float4*>(Ut + (tj0 * 32 + 32 + il) * kT2K + (kOB / 2) * h + 4 * sg);
+  for (int j = 0; j < 4; ++j)
 #pragma unroll
-      for (int s4 = 0; s4 < 4; ++s4) {
-        u0 = __builtin_amdgcn_mfma_f32_32x32x2f32(get4(fa, s4), get4(f0, s4), u0, 0, 0, 0);
-        u1 = __builtin_amdgcn_mfma_f32_32x32x2f32(get4(fa, s4), get4(f1, s4), u1, 0, 0, 0);
+    for (int v = 0; v < 16; ++v) u[j][v] = 0.f;
+#pragma unroll
+  for (int pass = 0; pass < 2; ++pass) {
+    // pass-local k index kk in [0, 64): kk < 32 -> k = 32 pass + kk, else k = 64 + 32 pass + kk - 32
+    if (pass) __syncthreads();  // the first pass's tiles consumed
+    VT av[kAQ];
+    float4 lv[8];
+#pragma unroll
+    for (int q = 0; q < kAQ; ++q) {  // the pass's A12 rows (64 k x 128 columns), gathered
+      const int e = tid + NT * q, kk = e / CPR, col = cb + (e % CPR) * W;
+      const int k = kk < 32 ? 32 * pass + kk : 64 + 32 * pass + kk - 32;
+      const VT x = ldu(bsrc[k], min(col, N - W));
+      if constexpr (VEC) av[q] = col < N ? x : make_float4(0.f, 0.f, 0.f, 0.f);
+      else av[q] = col < N ? x : 0.f;
+    }
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {  // the pass's L11^-1 columns (128 rows x 64 k), 16-B pieces
+      const int e = tid + NT * q, i = e / 16, kk = (e % 16) * 4;
+      const int k = kk < 32 ? 32 * pass + kk : 64 + 32 * pass + kk - 32;
+      lv[q] = *reinterpret_cast<const float4*>(Lb + (size_t)i * kOB + k);
+    }
+#pragma unroll
+    for (int q = 0; q < kAQ; ++q) {
+      const int e = tid + NT * q, kk = e / CPR, cl = (e % CPR) * W;
+      if constexpr (VEC) {
+        Uh[(cl + 0) * kT2PK + kk] = av[q].x; Uh[(cl + 1) * kT2PK + kk] = av[q].y;
+        Uh[(cl + 2) * kT2PK + kk] = av[q].z; Uh[(cl + 3) * kT2PK + kk] = av[q].w;
+      } else {
+        Uh[cl * kT2PK + kk] = av[q];
       }
     }
-    __syncthreads();  // A12^T and L11^-1 consumed
-    // accumulator v <-> row ti*32 + 8(v/4) + 4h + v%4 of U12, column tj*32 + il of the strip
 #pragma unroll
-    for (int v = 0; v < 16; ++v) {
-      const int i = ti * 32 + 8 * (v >> 2) + 4 * h + (v & 3);
-      Ut[(tj0 * 32 + il) * kT2K + i] = u0[v];
-      Ut[(tj0 * 32 + 32 + il) * kT2K + i] = u1[v];
+    for (int q = 0; q < 8; ++q) {
+      const int e = tid + NT * q;
+      *reinterpret_cast<float4*>(Lh + (e / 16) * kT2PK + (e % 16) * 4) = lv[q];
+    }
+    __syncthreads();
+#pragma unroll 2
+    for (int sg = 0; sg < 8; ++sg) {
+      const float4 fa = *reinterpret_cast<const float4*>(Lh + (wave * 32 + il) * kT2PK + 32 * h + 4 * sg);
+      float4 fb[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) fb[j] = *reinterpret_cast<const float4*>(Uh + (j * 32 + il) * kT2PK + 32 * h + 4 * sg);
+#pragma unroll
+      for (int s4 = 0; s4 < 4; ++s4)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) u[j] = __builtin_amdgcn_mfma_f32_32x32x2f32(get4(fa, s4), get4(fb[j], s4), u[j], 0, 0, 0);
     }
   }
+  __syncthreads();  // the pass tiles consumed: U12^T over them
+  // accumulator v of tile j <-> U12 row 32w + 8(v/4) + 4h + v%4, strip column 32j + il
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int v = 0; v < 16; ++v) Ut[(j * 32 + il) * kT2K + wave * 32 + 8 * (v >> 2) + 4 * h + (v & 3)] = u[j][v];
   __syncthreads();
-  const int wr = (wave >> 2) * 32, wc = (wave & 3) * 32;
+  const int wc = wave * 32;
   float4 ub[kOB / 8];  // U12[64h + 4sg + 0..3][wc + il]: this wave's MFMA operand for every step
 #pragma unroll
   for (int sg = 0; sg < kOB / 8; ++sg)
     ub[sg] = *reinterpret_cast<const float4*>(Ut + (wc + il) * kT2K + (kOB / 2) * h + 4 * sg);
-  __syncthreads();  // Ut consumed: Ls from here on
+  __syncthreads();  // Ut consumed: Ls / Cb from here on
 
   // ---- main loop
   auto loadC = [&](int step, VT (&c)[kCQ]) {
-    const unsigned long long m = *reinterpret_cast<const unsigned long long*>(dbits + 2 * step);
+    const unsigned m = __builtin_amdgcn_readfirstlane(dbits[step]);
+    const int pre = __builtin_amdgcn_readfirstlane((int)dpre[step]);
+    int srow[kCQ];
+#pragma unroll
+    for (int q = 0; q < kCQ; ++q) {  // (every lane reads a table entry: no branch around the loads)
+      const int ro = (tid + NT * q) / CPR;
+      srow[q] = dsrc[(pre + __builtin_popcount(m & ((1u << ro) - 1u))) & (kPermMax - 1)];
+    }
 #pragma unroll
     for (int q = 0; q < kCQ; ++q) {
       const int e = tid + NT * q, ro = e / CPR, row = c0 + step * kT2S + ro, col = cb + (e % CPR) * W;
-      c[q] = ldu(min(src_row(row, ro, m), N - 1), min(col, N - W));
+      const int src = ((m >> ro) & 1u) ? srow[q] : row;
+      c[q] = ldu(min(src, N - 1), min(col, N - W));
     }
   };
   auto loadL = [&](int step, VT (&l)[kLQ]) {
@@ -1028,27 +1043,65 @@ __global__ __launch_bounds__(kT2Threads, 1) void lu_trail128_kernel(int N, int P
 #pragma unroll
     for (int q = 0; q < kLQ; ++q) {
       const int e = tid + NT * q;
-      st_lds(Ls + (e / LPR) * kT2K + (e % LPR) * W, l[q]);
+      if constexpr (VEC) *reinterpret_cast<float4*>(Ls + (e / LPR) * kT2K + (e % LPR) * W) = l[q];
+      else Ls[(e / LPR) * kT2K + (e % LPR)] = l[q];
     }
   };
   // (the result overwrites c in place and is stored from there: a store's data registers stay busy
   // until the store completes, and c is not reloaded until the next step but one)
   auto storeOut = [&](int step, const float* Cb, VT (&c)[kCQ]) {
+    VT pr[kCQ];  // every product read before the first subtract: one LDS latency, not kCQ
+#pragma unroll
+    for (int q = 0; q < kCQ; ++q) {
+      const int e = tid + NT * q;
+      const float* src = Cb + (e / CPR) * kT2CS + (e % CPR) * W;
+      if constexpr (VEC) pr[q] = *reinterpret_cast<const float4*>(src);
+      else pr[q] = *src;
+    }
+    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int q = 0; q < kCQ; ++q) {
       const int e = tid + NT * q, row = c0 + step * kT2S + e / CPR, col = cb + (e % CPR) * W;
-      const float* src = Cb + (e / CPR) * kT2CS + (e % CPR) * W;
       if constexpr (VEC) {
-        const float4 pr = *reinterpret_cast<const float4*>(src);
-        c[q].x -= pr.x; c[q].y -= pr.y; c[q].z -= pr.z; c[q].w -= pr.w;
+        c[q].x -= pr[q].x; c[q].y -= pr[q].y; c[q].z -= pr[q].z; c[q].w -= pr[q].w;
       } else {
-        c[q] -= *src;
+        c[q] -= pr[q];
       }
       if (row < N && col < N) {
         if constexpr (VEC) *reinterpret_cast<float4*>(Ab + (size_t)row * N + col) = c[q];
         else Ab[(size_t)row * N + col] = c[q];
       }
     }
+  };
+  auto chain = [&](const float* Ls) -> floatx16 {
+    floatx16 acc = {};
+    if constexpr (DIAG != 1) {
+      // L21 fragments read two k-groups ahead of their MFMAs (pinned: the scheduler otherwise waits
+      // for each read right before its four MFMAs)
+      const floatx16 zero = {};  // the first MFMA takes an inline-zero C operand (no zeroing moves)
+      const float* lrow = Ls + il * kT2K + (kOB / 2) * h;
+      float4 fa[kOB / 8];
+      __builtin_amdgcn_sched_barrier(0);
+      fa[0] = *reinterpret_cast<const float4*>(lrow);
+      fa[1] = *reinterpret_cast<const float4*>(lrow + 4);
+#pragma unroll
+      for (int sg = 0; sg < kOB / 8; ++sg) {
+        if (sg + 2 < kOB / 8) fa[sg + 2] = *reinterpret_cast<const float4*>(lrow + 4 * (sg + 2));
+#pragma unroll
+        for (int s4 = 0; s4 < 4; ++s4)
+          acc = __builtin_amdgcn_mfma_f32_32x32x2f32(get4(fa[sg], s4), get4(ub[sg], s4), (sg == 0 && s4 == 0) ? zero : acc,
+                                                     0, 0, 0);
+      }
+      __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+#pragma unroll
+      for (int sg = 0; sg < kOB / 8 - 2; ++sg) {
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
+      }
+      __builtin_amdgcn_sched_group_barrier(0x008, 8, 0);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    return acc;
   };
 
   // step t (cc = A22 (t), loaded during step t - 1; lw = L21 (t + 1), loaded during step t - 1)
@@ -1059,19 +1112,9 @@ __global__ __launch_bounds__(kT2Threads, 1) void lu_trail128_kernel(int N, int P
       loadC(step + 1, cn);
       loadL(step + 2, lnext);
     }
-    floatx16 acc;
+    const floatx16 acc = chain(Ls);
 #pragma unroll
-    for (int v = 0; v < 16; ++v) acc[v] = 0.f;
-    if constexpr (DIAG != 1) {
-#pragma unroll
-      for (int sg = 0; sg < kOB / 8; ++sg) {
-        const float4 fa = *reinterpret_cast<const float4*>(Ls + (wr + il) * kT2K + (kOB / 2) * h + 4 * sg);
-#pragma unroll
-        for (int s4 = 0; s4 < 4; ++s4) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(get4(fa, s4), get4(ub[sg], s4), acc, 0, 0, 0);
-      }
-    }
-#pragma unroll
-    for (int v = 0; v < 16; ++v) Cb[(wr + 8 * (v >> 2) + 4 * h + (v & 3)) * kT2CS + wc + il] = acc[v];
+    for (int v = 0; v < 16; ++v) Cb[(8 * (v >> 2) + 4 * h + (v & 3)) * kT2CS + wc + il] = acc[v];
     writeL(Ls0 + ((step + 1) & 1) * (kT2S * kT2K), lw);
     __syncthreads();  // Cb[t & 1] = product (t), Ls[(t + 1) & 1] = L21 (t + 1); Ls[t & 1] consumed
     if (DIAG != 2) storeOut(step, Cb, cc);
@@ -1102,21 +1145,10 @@ __global__ __launch_bounds__(kT2Threads, 1) void lu_trail128_kernel(int N, int P
     loadL(1, l);
     __syncthreads();
     for (int step = 0; step < nsteps; ++step) {
-      const float* Ls = Ls0 + (step & 1) * (kT2S * kT2K);
       float* Cb = Cb0 + (step & 1) * (kT2S * kT2CS);
-      floatx16 acc;
+      const floatx16 acc = chain(Ls0 + (step & 1) * (kT2S * kT2K));
 #pragma unroll
-      for (int v = 0; v < 16; ++v) acc[v] = 0.f;
-      if constexpr (DIAG != 1) {
-#pragma unroll
-        for (int sg = 0; sg < kOB / 8; ++sg) {
-          const float4 fa = *reinterpret_cast<const float4*>(Ls + (wr + il) * kT2K + (kOB / 2) * h + 4 * sg);
-#pragma unroll
-          for (int s4 = 0; s4 < 4; ++s4) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(get4(fa, s4), get4(ub[sg], s4), acc, 0, 0, 0);
-        }
-      }
-#pragma unroll
-      for (int v = 0; v < 16; ++v) Cb[(wr + 8 * (v >> 2) + 4 * h + (v & 3)) * kT2CS + wc + il] = acc[v];
+      for (int v = 0; v < 16; ++v) Cb[(8 * (v >> 2) + 4 * h + (v & 3)) * kT2CS + wc + il] = acc[v];
       writeL(Ls0 + ((step + 1) & 1) * (kT2S * kT2K), l);
       __syncthreads();
       if (DIAG != 2) {
@@ -1129,8 +1161,7 @@ __global__ __launch_bounds__(kT2Threads, 1) void lu_trail128_kernel(int N, int P
   __syncthreads();  // every gathered load of a block row has completed: U12 to the block rows
   if (cb + wc + il < N) {
 #pragma unroll
-    for (int sg = 0; sg < kOB / 8; ++sg) {  // (static register index: the two waves with the same
-      if ((sg >= kOB / 16) != (wave >= 4)) continue;  //  columns split the rows)
+    for (int sg = 0; sg < kOB / 8; ++sg) {
       const int i = (kOB / 2) * h + 4 * sg;
       float* dst = Ab + (size_t)(P + i) * N + cb + wc + il;
       dst[0] = ub[sg].x;
@@ -1439,7 +1470,7 @@ extern "C" int iadmm_lu_solve(int64_t B, int64_t N, const float* LU, const int* 
   IADMM_ALLOW_LDS(lu_solve_kernel<true>, lds);
   IADMM_ALLOW_LDS(lu_solve_kernel<false>, lds);
   int dev = 0, cus = 256;
-  if (hipGetDevice(&dev) == hipSuccess) hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
   IADMM_ALLOW_LDS((lu_solve_kernel<true, 512>), lds);
   IADMM_ALLOW_LDS((lu_solve_kernel<true, 1024>), lds);
   if (N % 4 == 0 && aligned16(LU) && B <= cus)

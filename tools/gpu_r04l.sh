@@ -1,0 +1,13 @@
+#!/bin/bash
+# r04 session 8: paired trailing update in the factorization: A/B vs the r03 kernel (factor time,
+# bitwise fingerprint, backward error), the trailing microbenchmark, then the Stage-II tests
+set -o pipefail
+mkdir -p gpurun_out
+timeout -k 10 300 ./tools/lubench128.bin 1024 2000 > gpurun_out/r04l_lubench128.txt 2>&1 || exit $?
+grep -v "^$" gpurun_out/r04l_lubench128.txt | head -40
+timeout -k 10 400 python -u tools/lu_ab.py --libs variants/lu_r03trail.so i-admm-lstm_amd/iadmm/libiadmm.so variants/lu_r03trail.so i-admm-lstm_amd/iadmm/libiadmm.so > gpurun_out/r04l_lu_ab.txt 2>&1 || exit $?
+grep '^{' gpurun_out/r04l_lu_ab.txt | python3 -c "
+import sys,json
+for l in sys.stdin:
+    r=json.loads(l); print(r['lib'].split('/')[-1], round(r['best_ms'],2), round(r['frac_fp32_mfma'],3), r['lu_bits_sum'], r['piv_sum'], r['backward_error'])"
+bash tools/gpu_tests.sh r04l 900 tests/test_stage2_gpu.py tests/test_k100_gpu.py tests/test_config4_gpu.py tests/test_dropin_gpu.py || exit $?
