@@ -200,7 +200,9 @@ IADMM_DEV void panel_finish(float* Ab, int N, int K0, int k0, int nb, int cend, 
 // registers (an 8-wide panel keeps 10 rows per thread within the 128 VGPRs a 1024-thread
 // workgroup allows; 12 rows spill), so the pivot search still sees the whole column without
 // leaving registers.
-template <int M, int NB, int NT>
+// DIAG (tools/lupanelbench.hip only): 1 = no column steps (identity interchanges), 2 = no
+// panel_finish, 3 = neither (the panel's load and store alone).
+template <int M, int NB, int NT, int DIAG = 0>
 __global__ __launch_bounds__(NT, NT <= 256 ? (M <= 6 ? 4 : 2) : 1) void lu_panel_kernel(int N, int K0, int k0, int cend, float* A,
                                                                          int* piv, int* info) {
   constexpr int kNB = NB, kLuThreads = NT, NWV = NT / 64;
@@ -220,27 +222,76 @@ __global__ __launch_bounds__(NT, NT <= 256 ? (M <= 6 ? 4 : 2) : 1) void lu_panel
   const bool vec = nb == kNB && (N % 4) == 0 && aligned16(Ab);
 
   float a[M][kNB];
+  // STAGED (16-wide panels on 256 threads, 16-B aligned rows): the panel moves between HBM and the
+  // registers through a wave-private LDS stage, 16 rows x 64 B per memory instruction (four lanes
+  // per row) instead of 64 rows x 16 B: a row-per-lane access touches 64 cache lines per
+  // instruction with half of each used, and the load + store of the panel alone took 94 of the
+  // 116 us of a 1472-row launch (tools/lupanelbench.hip, profiles/r04_lupanelbench.txt).  Rows come
+  // in by LDS-DMA (no staging registers), two 64-row blocks per wave in flight; in the stage, the
+  // 16-B chunk c of block row r sits at position c ^ ((r >> 2) & 3) (conflict-free row reads).
+  constexpr bool STAGED = NT == 256 && NB == 16;
+  __shared__ __attribute__((aligned(16))) float pst[STAGED ? NWV : 1][2][STAGED ? 64 * kNB : 1];
+  typedef float f4v __attribute__((ext_vector_type(4)));
+  typedef __attribute__((address_space(3))) const f4v lds_cf4;
+  typedef __attribute__((address_space(3))) f4v lds_f4;
+  const bool staged = STAGED && vec;
+  // rows >= R read as zero (every use below is masked); the range ends at the panel's last row
+  const __amdgpu_buffer_rsrc_t prs =
+      __builtin_amdgcn_make_buffer_rsrc(Ab + (size_t)k0 * N + k0, 0, ((R - 1) * N + kNB) * 4, 0x00020000);
+  if (staged) {
+    // lane l of instruction i of block m: block row 16 i + (l >> 2), stage position l & 3, source
+    // chunk (l & 3) ^ ((l >> 4) & 3)
+    const unsigned vo = (unsigned)(((wave * 64 + (lane >> 2)) * N + 4 * ((lane & 3) ^ ((lane >> 4) & 3))) * 4);
+    auto issue = [&](int m) {
 #pragma unroll
-  for (int m = 0; m < M; ++m) {
-    const int r = tid + kLuThreads * m;
-    const float* src = Ab + (size_t)(k0 + min(r, R - 1)) * N + k0;
-    if (vec) {
+      for (int i = 0; i < 4; ++i)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(prs, (lds_void*)(&pst[wave][m & 1][i * 256]), 16, vo,
+                                                 (kLuThreads * m + 16 * i) * N * 4, 0, 0);
+    };
+    const unsigned rb = (unsigned)(uintptr_t)(lds_cf4*)(const f4v*)&pst[wave][0][lane * kNB];
+    const int sr = (lane >> 2) & 3;
+    issue(0);
+    if (M > 1) issue(1);
 #pragma unroll
-      for (int c4 = 0; c4 < kNB; c4 += 4) {
-        const float4 v = *reinterpret_cast<const float4*>(src + c4);
-        a[m][c4] = v.x; a[m][c4 + 1] = v.y; a[m][c4 + 2] = v.z; a[m][c4 + 3] = v.w;
+    for (int m = 0; m < M; ++m) {
+      if (m + 1 < M) vm_wait<4>(); else vm_wait<0>();  // block m landed (block m + 1 may be in flight)
+      const unsigned ra = rb + (unsigned)((m & 1) * 64 * kNB * 4);
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const f4v v = *(lds_cf4*)(uintptr_t)(ra + (unsigned)(((c ^ sr) * 4) * 4));
+        a[m][4 * c] = v.x; a[m][4 * c + 1] = v.y; a[m][4 * c + 2] = v.z; a[m][4 * c + 3] = v.w;
       }
-    } else {
-#pragma unroll
-      for (int c = 0; c < kNB; ++c) a[m][c] = src[min(c, nb - 1)];
+      if (m + 2 < M) {
+        __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this buffer's reads done before it refills
+        issue(m + 2);
+      }
     }
-    // (no zero fill of rows >= R / columns >= nb: every use below is masked, and overwriting a
-    // register a load is still filling would stall on that load right here)
+  } else {
+#pragma unroll
+    for (int m = 0; m < M; ++m) {
+      const int r = tid + kLuThreads * m;
+      const float* src = Ab + (size_t)(k0 + min(r, R - 1)) * N + k0;
+      if (vec) {
+#pragma unroll
+        for (int c4 = 0; c4 < kNB; c4 += 4) {
+          const float4 v = *reinterpret_cast<const float4*>(src + c4);
+          a[m][c4] = v.x; a[m][c4 + 1] = v.y; a[m][c4 + 2] = v.z; a[m][c4 + 3] = v.w;
+        }
+      } else {
+#pragma unroll
+        for (int c = 0; c < kNB; ++c) a[m][c] = src[min(c, nb - 1)];
+      }
+      // (no zero fill of rows >= R / columns >= nb: every use below is masked, and overwriting a
+      // register a load is still filling would stall on that load right here)
+    }
   }
 
+  if constexpr (DIAG & 1) {
+    if (tid < kNB) pvs[tid] = k0 + tid;
+  }
 #pragma unroll
   for (int j = 0; j < kNB; ++j) {
-    if (j < nb) {
+    if (!(DIAG & 1) && j < nb) {
       const int q = j & 1;
       float best = -1.f;
       int bi = R;
@@ -315,10 +366,38 @@ __global__ __launch_bounds__(NT, NT <= 256 ? (M <= 6 ? 4 : 2) : 1) void lu_panel
   }
 
   // write the factored panel back; L11 for the in-block substitution
+  if (staged) {  // through the stage: own row in, 16 rows x 64 B out per store instruction
+    const unsigned wb = (unsigned)(uintptr_t)(lds_f4*)(f4v*)&pst[wave][0][0];
+    const int sr = (lane >> 2) & 3;
+    const unsigned vo = (unsigned)(((wave * 64 + (lane >> 2)) * N + 4 * ((lane & 3) ^ ((lane >> 4) & 3))) * 4);
+#pragma unroll
+    for (int m = 0; m < M; ++m) {
+      const unsigned bb = wb + (unsigned)((m & 1) * 64 * kNB * 4);
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+        *(lds_f4*)(uintptr_t)(bb + (unsigned)((lane * kNB + (c ^ sr) * 4) * 4)) =
+            f4v{a[m][4 * c], a[m][4 * c + 1], a[m][4 * c + 2], a[m][4 * c + 3]};
+      f4v o[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) o[i] = *(lds_cf4*)(uintptr_t)(bb + (unsigned)((i * 256 + lane * 4) * 4));
+      // every value in registers before the first store, and the stores drained before the next
+      // block's LDS reads: an LDS return into the registers of a store still in flight made the
+      // factors nondeterministic (the compiler reuses them; profiles/r04_lupanelbench_staged.txt).
+      // Draining costs nothing measurable (same file: 121-123 vs 126-129 us at 1984 rows).
+      __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        __builtin_amdgcn_raw_buffer_store_b128(
+            __builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, o[i]), prs, vo, (kLuThreads * m + 16 * i) * N * 4, 0);
+      vm_wait<0>();
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
 #pragma unroll
   for (int m = 0; m < M; ++m) {
     const int r = tid + kLuThreads * m;
-    if (r < R) {
+    if (!staged && r < R) {
       float* dst = Ab + (size_t)(k0 + r) * N + k0;
       if (vec) {
 #pragma unroll
@@ -335,7 +414,7 @@ __global__ __launch_bounds__(NT, NT <= 256 ? (M <= 6 ? 4 : 2) : 1) void lu_panel
 #pragma unroll
     for (int c = 0; c < kNB; ++c) L11[tid][c] = a[0][c];
   }
-  panel_finish<kNB>(Ab, N, K0, k0, nb, cend, L11, pvs, prow, pcur, pcnt);
+  if constexpr (!(DIAG & 2)) panel_finish<kNB>(Ab, N, K0, k0, nb, cend, L11, pvs, prow, pcur, pcnt);
 }
 
 // Global-memory panel for N > 10240 (rows beyond what the register panel can hold, up to the
