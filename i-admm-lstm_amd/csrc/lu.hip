@@ -34,6 +34,7 @@
 // row piv[i]-1), so (LU, piv) also feeds torch.linalg.lu_solve.  info[b] = first i+1 with a zero
 // pivot (0 = non-singular), LAPACK convention.
 #include <algorithm>
+#include <cstdlib>
 #include <type_traits>
 
 #include "common.h"
@@ -93,6 +94,7 @@ constexpr int kBigNB = 8;          // panel width above N = 8 * 256
 constexpr int kBigThreads = 1024;  // panel workgroup size above N = 8 * 256
 constexpr int kBigMaxM = 10;       // rows per thread there: N <= 10 * 1024 (12 spills at 128 VGPRs)
 constexpr int kLuMaxN = 36736;     // = lu_solve's LDS limit; panels past 10240 rows run from HBM
+constexpr int kLuMaxHbmN = 46340;  // above kLuMaxN: x in HBM, interchanges as a pass (N * N < 2^31)
 constexpr int kLuThreads = 256;
 constexpr int kUpdRows = 64;
 constexpr int kSolveBlk = 64;
@@ -1010,7 +1012,8 @@ __global__ __launch_bounds__(kT2Threads, 2) void lu_trail128_kernel(int N, int P
     const int* pb = perm + b * kPermInts;
     if (tid < kOB) bsrc[tid] = perm ? pb[2 * kPermMax + tid] : P + tid;
     if (tid < ndisp) { tdst[tid] = pb[kOB + tid]; tsrc[tid] = pb[2 * kPermMax + kOB + tid]; }
-    for (int w = tid; w < nsteps + 2; w += NT) { dbits[w] = 0u; dpre[w] = 0; }  // (+ one past the end)
+    if (perm)  // (the tables are sized for N <= kLuMaxN: the interchange-free form never reads them)
+      for (int w = tid; w < nsteps + 2; w += NT) { dbits[w] = 0u; dpre[w] = 0; }  // (+ one past the end)
   }
   __syncthreads();
   int drank = 0, dd = 0;
@@ -1096,8 +1099,8 @@ __global__ __launch_bounds__(kT2Threads, 2) void lu_trail128_kernel(int N, int P
 
   // ---- main loop
   auto loadC = [&](int step, VT (&c)[kCQ]) {
-    const unsigned m = __builtin_amdgcn_readfirstlane(dbits[step]);
-    const int pre = __builtin_amdgcn_readfirstlane((int)dpre[step]);
+    const unsigned m = perm ? __builtin_amdgcn_readfirstlane(dbits[step]) : 0u;
+    const int pre = perm ? __builtin_amdgcn_readfirstlane((int)dpre[step]) : 0;
     int srow[kCQ];
 #pragma unroll
     for (int q = 0; q < kCQ; ++q) {  // (every lane reads a table entry: no branch around the loads)
@@ -1477,7 +1480,7 @@ static int lu_rank64(int64_t B, int64_t N, int K0, int cend, int cmax, float* A,
 }
 
 static int lu_factor_blocks(int64_t B, int64_t N, float* A, int* piv, int* info, int* perm, float* linv,
-                            hipStream_t s) {
+                            hipStream_t s, bool gather) {
   const bool vec = (N % 4 == 0) && aligned16(A);
   IADMM_ALLOW_LDS(lu_trail_kernel<true>, kTrailLds);
   IADMM_ALLOW_LDS((lu_trail_kernel<true, 0, kTC / 2>), kTrailLds);
@@ -1497,22 +1500,156 @@ static int lu_factor_blocks(int64_t B, int64_t N, float* A, int* piv, int* info,
     if (!rc && c1 < n_) rc = lu_factor_half(B, N, c1, c2, A, piv, info, s);
     if (!rc && c1 < n_) rc = lu_swap(B, N, c1, c2, P, c1, 0, 0, 0, A, piv, perm, s);
     // the whole block's interchanges composed into one row permutation: applied here to the columns
-    // left of the block, and inside lu_trail128_kernel (gathered loads) to the columns right of it
+    // left of the block, and inside lu_trail128_kernel (gathered loads) to the columns right of it --
+    // or here too (gather = false: N above the trailing kernel's LDS tables), then an
+    // interchange-free trailing update
     if (rc) break;
     hipLaunchKernelGGL(lu_block_perm_kernel, dim3((unsigned)B), dim3(64), 0, s, (int)N, P, c2, piv, perm);
     IADMM_CHECK_LAUNCH();
-    rc = lu_swap(B, N, P, c2, 0, P, 0, 0, 0, A, piv, perm, s, false);
+    rc = lu_swap(B, N, P, c2, 0, P, gather ? 0 : c2, gather ? 0 : n_, 0, A, piv, perm, s, false);
     if (rc || c2 >= n_) break;
     // U12 = L11^-1 A12 and the rank-128 update of everything right of the block
     hipLaunchKernelGGL(lu_linv_kernel, dim3((unsigned)B), dim3(kOB), 0, s, (int)N, P, A, linv);
     IADMM_CHECK_LAUNCH();
     const int ntc = ((int)N - c2 + kT2C - 1) / kT2C;
     const dim3 grid((unsigned)(B * ntc));
-    if (vec) hipLaunchKernelGGL(lu_trail128_kernel<true>, grid, dim3(kT2Threads), kT2Lds, s, (int)N, P, ntc, A, linv, perm);
-    else hipLaunchKernelGGL(lu_trail128_kernel<false>, grid, dim3(kT2Threads), kT2Lds, s, (int)N, P, ntc, A, linv, perm);
+    const int* gp = gather ? perm : nullptr;
+    if (vec) hipLaunchKernelGGL(lu_trail128_kernel<true>, grid, dim3(kT2Threads), kT2Lds, s, (int)N, P, ntc, A, linv, gp);
+    else hipLaunchKernelGGL(lu_trail128_kernel<false>, grid, dim3(kT2Threads), kT2Lds, s, (int)N, P, ntc, A, linv, gp);
     IADMM_CHECK_LAUNCH();
   }
   return rc;
+}
+
+// ---- Solve with x in HBM (N above the LDS-resident lu_solve_kernel's limit, r04) ----
+// P b, then forward (unit L) and backward (U) substitution in 64-row blocks, right-looking: per
+// block one launch solves the diagonal block (one wave per instance, the block in LDS) and one
+// launch subtracts its contribution from every remaining row (lu_solve_gemv_kernel: 64 rows per
+// workgroup, 16 lanes per row, all workgroups of the grid streaming the block column).  Launch-bound
+// (four launches per block pair), but every CU streams the factors, which one workgroup per
+// instance could not at the batch sizes such N leaves room for.
+
+// P b: each 64-row block's interchanges composed (build_row_perm) and applied with every load
+// before every store; one wave per instance walks the blocks in order.
+__global__ __launch_bounds__(64) void lu_solve_perm_kernel(int N, const int* piv, float* X) {
+  __shared__ int pvs[kSolveBlk], prow[2 * kSolveBlk], pcur[2 * kSolveBlk], pcnt[1];
+  const int lane = threadIdx.x;
+  const size_t b = blockIdx.x;
+  float* x = X + b * N;
+  for (int k0 = 0; k0 < N; k0 += kSolveBlk) {
+    const int nbk = min(kSolveBlk, N - k0);
+    if (lane < nbk) pvs[lane] = piv[b * N + k0 + lane] - 1;
+    __syncthreads();
+    build_row_perm(pvs, k0, nbk, prow, pcur, pcnt);
+    const int cnt = *pcnt;
+    const float v0 = x[pcur[min(lane, cnt - 1)]], v1 = x[pcur[min(lane + 64, cnt - 1)]];
+    if (lane < cnt) x[prow[lane]] = v0;
+    if (lane + 64 < cnt) x[prow[lane + 64]] = v1;
+    __syncthreads();  // (the stores ordered before the next block's loads; LDS tables reused)
+  }
+}
+
+// x[k0, k1) <- (unit lower | upper) triangle of the diagonal block \ x[k0, k1); one wave per instance.
+template <bool UPPER>
+__global__ __launch_bounds__(64) void lu_solve_tri_kernel(int N, const float* LU, float* X, int k0) {
+  __shared__ float D[kSolveBlk][kSolveBlk + 1];
+  const int lane = threadIdx.x;
+  const size_t b = blockIdx.x;
+  const float* M = LU + b * (size_t)N * N;
+  float* x = X + b * N;
+  const int nbk = min(kSolveBlk, N - k0);
+  const int c = min(lane, nbk - 1);
+  float d[kSolveBlk];
+#pragma unroll
+  for (int r = 0; r < kSolveBlk; ++r) d[r] = M[(size_t)(k0 + min(r, nbk - 1)) * N + k0 + c];  // all in flight
+#pragma unroll
+  for (int r = 0; r < kSolveBlk; ++r) D[r][lane] = d[r];
+  __syncthreads();
+  float v = lane < nbk ? x[k0 + lane] : 0.f;
+  if (!UPPER) {
+    for (int j = 0; j < nbk; ++j) {
+      const float xj = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), j));
+      if (lane > j && lane < nbk) v = fmaf(-D[lane][j], xj, v);
+    }
+  } else {
+    for (int j = nbk - 1; j >= 0; --j) {
+      const float vj = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), j)) / D[j][j];
+      if (lane == j) v = vj;
+      if (lane < j) v = fmaf(-D[lane][j], vj, v);
+    }
+  }
+  if (lane < nbk) x[k0 + lane] = v;
+}
+
+// x[r] -= M[r, k0:k1) . x[k0:k1) for r in [r0, r1): 64 rows per workgroup (grid (B, row blocks)),
+// 4 rows per wave at a time, lane (row, q = lane & 15) holding columns 4q .. 4q + 3 of the block.
+template <bool VEC>
+__global__ __launch_bounds__(256) void lu_solve_gemv_kernel(int N, const float* LU, float* X, int k0, int r0, int r1) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, q = lane & 15;
+  const size_t b = blockIdx.x;
+  const float* M = LU + b * (size_t)N * N;
+  float* x = X + b * N;
+  const int nbk = min(kSolveBlk, N - k0);
+  float xv[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) xv[e] = 4 * q + e < nbk ? x[k0 + 4 * q + e] : 0.f;
+  const int rbase = r0 + blockIdx.y * 64 + wave * 16;
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    const int r = rbase + 4 * g + (lane >> 4);
+    const int rr = min(r, r1 - 1);
+    const float* row = M + (size_t)rr * N + k0 + 4 * q;
+    float a[4];
+    if (VEC && 4 * q + 3 < nbk) {
+      const float4 t = *reinterpret_cast<const float4*>(row);
+      a[0] = t.x; a[1] = t.y; a[2] = t.z; a[3] = t.w;
+    } else {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) a[e] = 4 * q + e < nbk ? row[min(e, nbk - 1 - 4 * q)] : 0.f;
+    }
+    float sum = fmaf(a[3], xv[3], fmaf(a[2], xv[2], fmaf(a[1], xv[1], a[0] * xv[0])));
+#pragma unroll
+    for (int off = 8; off >= 1; off >>= 1) sum += __shfl_xor(sum, off, 16);
+    if (q == 0 && r < r1) x[r] -= sum;
+  }
+}
+
+// (test hook: IADMM_LU_FORCE_HBM=1 sends every size through the HBM forms -- the interchange pass
+// instead of the gathered trailing-update loads, and the multi-launch solve -- so tests can compare
+// them with the LDS-resident forms at sizes that have both)
+static bool lu_force_hbm() {
+  const char* e = getenv("IADMM_LU_FORCE_HBM");
+  return e && e[0] == '1';
+}
+
+static int lu_solve_hbm(int64_t B, int64_t N, const float* LU, const int* piv, float* x, hipStream_t s) {
+  const bool vec = N % 4 == 0 && aligned16(LU);
+  hipLaunchKernelGGL(lu_solve_perm_kernel, dim3((unsigned)B), dim3(64), 0, s, (int)N, piv, x);
+  IADMM_CHECK_LAUNCH();
+  const int nblk = (int)((N + kSolveBlk - 1) / kSolveBlk);
+  for (int bb = 0; bb < nblk; ++bb) {  // forward, unit L
+    const int k0 = bb * kSolveBlk, k1 = std::min((int)N, k0 + kSolveBlk);
+    hipLaunchKernelGGL(lu_solve_tri_kernel<false>, dim3((unsigned)B), dim3(64), 0, s, (int)N, LU, x, k0);
+    IADMM_CHECK_LAUNCH();
+    if (k1 < N) {
+      const dim3 g((unsigned)B, (unsigned)((N - k1 + 63) / 64));
+      if (vec) hipLaunchKernelGGL(lu_solve_gemv_kernel<true>, g, dim3(256), 0, s, (int)N, LU, x, k0, k1, (int)N);
+      else hipLaunchKernelGGL(lu_solve_gemv_kernel<false>, g, dim3(256), 0, s, (int)N, LU, x, k0, k1, (int)N);
+      IADMM_CHECK_LAUNCH();
+    }
+  }
+  for (int bb = nblk - 1; bb >= 0; --bb) {  // backward, U
+    const int k0 = bb * kSolveBlk;
+    hipLaunchKernelGGL(lu_solve_tri_kernel<true>, dim3((unsigned)B), dim3(64), 0, s, (int)N, LU, x, k0);
+    IADMM_CHECK_LAUNCH();
+    if (k0 > 0) {
+      const dim3 g((unsigned)B, (unsigned)((k0 + 63) / 64));
+      if (vec) hipLaunchKernelGGL(lu_solve_gemv_kernel<true>, g, dim3(256), 0, s, (int)N, LU, x, k0, 0, k0);
+      else hipLaunchKernelGGL(lu_solve_gemv_kernel<false>, g, dim3(256), 0, s, (int)N, LU, x, k0, 0, k0);
+      IADMM_CHECK_LAUNCH();
+    }
+  }
+  return 0;
 }
 
 // workspace: per-instance block permutations (kPermInts ints) + the 128 x 128 L11^-1 of the current
@@ -1530,7 +1667,7 @@ extern "C" int iadmm_lu_factor(int64_t B, int64_t N, float* A, int* piv, int* in
   if (B <= 0 || N <= 0 || !A || !piv || !info || !ws) return IADMM_E_ARG;
   if (ws_bytes < lu_ws_bytes(B)) return IADMM_E_ARG;
   if (!aligned16(ws)) return IADMM_E_ALIGN;
-  if (N > kLuMaxN || B > 0x7fffffff) return IADMM_E_SIZE;
+  if (N > kLuMaxHbmN || B > 0x7fffffff) return IADMM_E_SIZE;
   const int64_t ntc_max = (N + kTC - 1) / kTC, nrc_max = (N + kTRW - 1) / kTRW;
   if (B * ntc_max * nrc_max > 0x7fffffff) return IADMM_E_SIZE;
   hipStream_t s = (hipStream_t)stream;
@@ -1538,14 +1675,16 @@ extern "C" int iadmm_lu_factor(int64_t B, int64_t N, float* A, int* piv, int* in
   if (e != hipSuccess) return (int)e;
   int* perm = static_cast<int*>(ws);
   float* linv = reinterpret_cast<float*>(static_cast<char*>(ws) + lu_perm_bytes(B));
-  return lu_factor_blocks(B, N, A, piv, info, perm, linv, s);
+  return lu_factor_blocks(B, N, A, piv, info, perm, linv, s, N <= kLuMaxN && !lu_force_hbm());
 }
 
 extern "C" int iadmm_lu_solve(int64_t B, int64_t N, const float* LU, const int* piv, float* x,
                               void* stream) {
   if (B <= 0 || N <= 0 || !LU || !piv || !x) return IADMM_E_ARG;
   const size_t lds = ((size_t)N + kSolveBlk + kSolveBlk * kDS) * sizeof(float);
-  if (lds > 160 * 1024 || B > 0x7fffffff) return IADMM_E_SIZE;  // gfx950: 160 KiB of LDS per workgroup
+  if (N > kLuMaxHbmN || B > 0x7fffffff || B * ((N + 63) / 64) > 0x7fffffff) return IADMM_E_SIZE;
+  // gfx950: 160 KiB of LDS per workgroup; x beyond it lives in HBM
+  if (lds > 160 * 1024 || lu_force_hbm()) return lu_solve_hbm(B, N, LU, piv, x, (hipStream_t)stream);
   IADMM_ALLOW_LDS(lu_solve_kernel<true>, lds);
   IADMM_ALLOW_LDS(lu_solve_kernel<false>, lds);
   int dev = 0, cus = 256;

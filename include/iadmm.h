@@ -112,7 +112,8 @@ int iadmm_kkt_rhs(int64_t B, int64_t n, int64_t m, int64_t num_ineq, const float
  * (row i was swapped with row piv[i]-1);
  * info[B] = first 1-based zero pivot or 0.  Right-looking in 128-column blocks (two 64-column halves; 16-column
  * panels up to N = 2048, 8-column panels on 1024-thread workgroups above, held in registers up to 10240 panel
- * rows and in HBM beyond; rank-128 MFMA trailing update; limit N <= 36736, the solve's).
+ * rows and in HBM beyond; rank-128 MFMA trailing update with the block's interchanges as gathered loads up to
+ * N = 36736, as a pass of their own above; limit N <= 46340, N * N < 2^31).
  * ws: caller-owned, 16-B aligned device workspace of at least iadmm_lu_factor_ws_bytes(B, N) bytes
  * (per-instance block permutations and the 128x128 L11^-1 blocks); nothing is allocated inside. */
 int64_t iadmm_lu_factor_ws_bytes(int64_t B, int64_t N);
@@ -120,7 +121,8 @@ int iadmm_lu_factor(int64_t B, int64_t N, float* A, int* piv, int* info, void* w
                     void* stream);
 
 /* Solve with the factors in place (replaces torch.lu_solve, models/lu.py:32,35): x[B,N] holds b
- * on entry and the solution on exit.  Limit: (N + 4224) floats of LDS <= 160 KiB, N <= 36736. */
+ * on entry and the solution on exit.  x lives in LDS while (N + 4224) floats fit 160 KiB (N <= 36736), in
+ * HBM above (several launches per 64-row block); limit N <= 46340. */
 int iadmm_lu_solve(int64_t B, int64_t N, const float* LU, const int* piv, float* x, void* stream);
 
 /* Pack the LSTM gate weights for the cell kernel (models/lstm.py:21-38 parameter layout).

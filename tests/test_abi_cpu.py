@@ -84,6 +84,18 @@ def test_lu_factor_workspace_is_caller_owned():
         _abi.call("iadmm_lu_factor", 2, 100, 16, 16, 16, 20, need, None)
 
 
+def test_lu_size_limit_is_the_hbm_forms():
+    """Stage II sizes (r04): above the LDS-resident solve's N = 36736 the HBM forms take over
+    (tests/test_lu_hbm_gpu.py runs N = 36800); both entry points refuse only N > 46340 (N * N must
+    stay below 2^31), before touching any pointer."""
+    lib = _abi.lib()
+    need = lib.iadmm_lu_factor_ws_bytes(1, 46341)
+    with pytest.raises(_abi.IadmmError, match="size beyond"):
+        _abi.call("iadmm_lu_factor", 1, 46341, 16, 16, 16, 16, need, None)
+    with pytest.raises(_abi.IadmmError, match="size beyond"):
+        _abi.call("iadmm_lu_solve", 1, 46341, 16, 16, 16, None)
+
+
 def test_no_device_allocation_inside_the_library():
     """Every device buffer is caller-owned: no hipMalloc* / hipFree* call in the HIP sources."""
     csrc = os.path.join(REPO, "i-admm-lstm_amd", "csrc")
