@@ -109,28 +109,50 @@ constexpr int kTrailThreads = 512;
 constexpr size_t kTrailLds = ((kTC + 2 * kTRS) * kTS + 2 * kTRS * kCS) * sizeof(float);
 
 // The net row permutation of n interchanges (row base + j <-> pv[j], in order, ?laswp):
-// afterwards row rowid[i] holds what row cur[i] held before, for i < *cnt (<= 2n; rowid[i] =
-// base + i for i < n).  Built by wave 0 in LDS (lane-parallel search with a ballot); the caller
-// moves each column with all loads before all stores, one memory latency instead of n.
+// afterwards row rowid[i] holds what row cur[i] held before, for i < *cnt (<= 2n <= 256; rowid[i] =
+// base + i for i < n).  Built by wave 0 with both lists in registers (entry i = lane i % 64 of slot
+// i / 64): per interchange a ballot search over the live slots and lane-indexed reads and writes,
+// no LDS round trip (r04: the LDS-resident lists cost ~500 cycles per interchange, ~30 us for a
+// 128-row block); the lists go to LDS once at the end.  The caller moves each column with all loads
+// before all stores, one memory latency instead of n.
 IADMM_DEV void build_row_perm(const int* pv, int base, int n, int* rowid, int* cur, int* cnt) {
   const int lane = threadIdx.x & 63;
   if ((threadIdx.x >> 6) == 0) {
-    for (int i = lane; i < n; i += 64) { rowid[i] = base + i; cur[i] = base + i; }
+    int rw[4], cr[4];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) rw[s] = cr[s] = base + 64 * s + lane;
+    const int pv0 = pv[min(lane, n - 1)], pv1 = pv[min(64 + lane, n - 1)];
     int c = n;
     for (int j = 0; j < n; ++j) {
-      const int p = pv[j];
+      const int p = __builtin_amdgcn_readlane(j < 64 ? pv0 : pv1, j & 63);
       if (p == base + j) continue;
       int found = -1;
-      for (int s0 = 0; s0 < c && found < 0; s0 += 64) {
-        const unsigned long long m = __ballot(s0 + lane < c && rowid[s0 + lane] == p);
-        if (m) found = s0 + __ffsll((long long)m) - 1;
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        if (found < 0 && 64 * s < c) {
+          const unsigned long long m = __ballot(rw[s] == p && 64 * s + lane < c);
+          if (m) found = 64 * s + __ffsll((long long)m) - 1;
+        }
       }
       if (found < 0) {
-        if (lane == 0) { rowid[c] = p; cur[c] = p; }
         found = c++;
+#pragma unroll
+        for (int s = 0; s < 4; ++s)
+          if (s == (found >> 6) && lane == (found & 63)) { rw[s] = p; cr[s] = p; }
       }
-      if (lane == 0) { const int t = cur[j]; cur[j] = cur[found]; cur[found] = t; }
+      const int sj = j >> 6, sf = found >> 6;
+      const int vj = sj == 0 ? cr[0] : (sj == 1 ? cr[1] : (sj == 2 ? cr[2] : cr[3]));
+      const int vf = sf == 0 ? cr[0] : (sf == 1 ? cr[1] : (sf == 2 ? cr[2] : cr[3]));
+      const int tj = __builtin_amdgcn_readlane(vj, j & 63), tf = __builtin_amdgcn_readlane(vf, found & 63);
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        if (s == sj && lane == (j & 63)) cr[s] = tf;
+        if (s == sf && lane == (found & 63)) cr[s] = tj;
+      }
     }
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+      if (64 * s + lane < c) { rowid[64 * s + lane] = rw[s]; cur[64 * s + lane] = cr[s]; }
     if (lane == 0) *cnt = c;
   }
   __syncthreads();
