@@ -14,8 +14,9 @@
 // per 128-column block: first half factored; its interchanges + U12 on the second half
 // (lu_swap_kernel<64, true>); the second half's rank-64 update (lu_trail_kernel, cmax); second
 // half factored; its interchanges on the first half; the block's 128 interchanges composed into
-// one row permutation (lu_block_perm_kernel) applied left and right of the block in one pass
-// (lu_swap_kernel<128, false>); L11^-1 (lu_linv_kernel); then
+// one row permutation (lu_block_perm_kernel), applied right of the block by the trailing update's
+// gathered loads and left of it at the end, all blocks in one pass (lu_left_compose_kernel +
+// lu_left_apply_kernel; N > 2048: per block, lu_swap_kernel<128, false>); L11^-1 (lu_linv_kernel); then
 //   lu_trail128_kernel     U12 = L11^-1 A12 (MFMA prologue) and A22 -= L21 U12 at rank 128 on fp32
 //                          MFMA (v_mfma_f32_32x32x2f32): 128-column strips streamed in 64-row
 //                          steps, A22 read + written once per 128 columns.
@@ -1419,6 +1420,81 @@ __global__ void kkt_rhs_kernel(int64_t B, int n, int m, int num_ineq, const floa
   }
 }
 
+// ---- The interchanges left of each block, deferred to one final pass (N <= 2048, r04) ----
+// ?getrf applies block t's interchanges to the columns [0, 128 t) as soon as block t is factored;
+// nothing reads those columns again before the solve, so each 128-column block j can instead take
+// the composition of all later blocks' interchanges at the end, once: its rows [128 (j + 1), N)
+// are read and written once (1 KB per row and block) instead of 256 rows per later block (~2x fewer
+// bytes at N = 2000: 15 MB instead of 31.5 MB per instance).  The factors are bit for bit those of
+// the per-block form (interchanges only move values).
+//
+// sigma_j[k] = the row that ends at position k of block j's columns: with pi_t the permutation of
+// block t (row rowid[i] takes what row cur[i] held, build_row_perm), applying pi_{j+1}, ..., pi_{nb-1}
+// in turn gives sigma_j = pi_{j+1} o sigma_{j+1}, sigma_{nb-1} = identity.  Kept with its inverse in
+// LDS, each step is a sparse update over the <= 256 rows pi_t moves.
+constexpr int kLeftDeferMaxN = 2048;  // rows below a block <= 1920: 15 float4 per thread at 1024 threads
+__host__ __device__ inline int64_t left_sig_off(int64_t N, int64_t j) { return j * N - (int64_t)kOB * j * (j + 1) / 2; }
+
+// one wave per instance: sigma_j on rows [128 (j + 1), N) for j = nb - 2 .. 0 into sig (per instance
+// left_sig_off(N, nb - 1) ints); perm = block t's permutation at perm + t * slot + b * kPermInts
+__global__ __launch_bounds__(64) void lu_left_compose_kernel(int N, int nb, int64_t slot, const int* perm, int* sig) {
+  __shared__ int sg[kLeftDeferMaxN], iv[kLeftDeferMaxN];
+  const int lane = threadIdx.x;
+  const size_t b = blockIdx.x;
+  for (int k = lane; k < N; k += 64) sg[k] = iv[k] = k;
+  __syncthreads();
+  int* out = sig + b * (size_t)left_sig_off(N, nb - 1);
+  for (int t = nb - 1; t >= 1; --t) {
+    const int* pb = perm + (size_t)t * slot + b * kPermInts;
+    const int cnt = pb[4 * kPermMax];
+    int kk[4], cc[4];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const int i = 64 * s + lane;
+      kk[s] = i < cnt ? iv[pb[i]] : -1;
+      cc[s] = i < cnt ? pb[2 * kPermMax + i] : -1;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+      if (kk[s] >= 0) { sg[kk[s]] = cc[s]; iv[cc[s]] = kk[s]; }
+    __syncthreads();
+    const int r0 = kOB * t;  // sigma_{t-1}: rows [128 t, N)
+    int* o = out + left_sig_off(N, t - 1);
+    for (int k = r0 + lane; k < N; k += 64) o[k - r0] = sg[k];
+  }
+}
+
+// rows [128 (j + 1), N) of a 32-column piece of block j take rows sigma_j (in place: every load of
+// the piece, then the workgroup's barrier, then every store).  Workgroup g: instance g % B, piece
+// (g / B) % 4 of block (g / B) / 4, the heavy blocks (small j) first.  VEC: 16-B accesses, 8 lanes
+// per row (a 128-B line per row and piece).
+template <bool VEC>
+__global__ __launch_bounds__(1024) void lu_left_apply_kernel(int N, int B, const int* sig, float* A) {
+  constexpr int kLpr = VEC ? 8 : 32, kRpp = 1024 / kLpr;
+  constexpr int kPass = (kLeftDeferMaxN - kOB + kRpp - 1) / kRpp;
+  typedef typename std::conditional<VEC, float4v, float>::type T;
+  const int g = blockIdx.x, b = g % B, jq = g / B, j = jq >> 2;
+  const int tid = threadIdx.x, rr = tid / kLpr;
+  const int c = kOB * j + 32 * (jq & 3) + (VEC ? 4 : 1) * (tid % kLpr);
+  const int r0 = kOB * (j + 1), R = N - r0;
+  const int* sg = sig + (size_t)b * left_sig_off(N, (N + kOB - 1) / kOB - 1) + left_sig_off(N, j);
+  float* Ab = A + (size_t)b * N * N;
+  T v[kPass];
+#pragma unroll
+  for (int p = 0; p < kPass; ++p) {
+    const int src = sg[min(p * kRpp + rr, R - 1)];
+    v[p] = *reinterpret_cast<const T*>(Ab + (size_t)src * N + c);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+#pragma unroll
+  for (int p = 0; p < kPass; ++p) {
+    const int r = p * kRpp + rr;
+    if (r < R) *reinterpret_cast<T*>(Ab + (size_t)(r0 + r) * N + c) = v[p];
+  }
+}
+
 }  // namespace iadmm
 
 using namespace iadmm;
@@ -1501,7 +1577,7 @@ static int lu_rank64(int64_t B, int64_t N, int K0, int cend, int cmax, float* A,
   return 0;
 }
 
-static int lu_factor_blocks(int64_t B, int64_t N, float* A, int* piv, int* info, int* perm, float* linv,
+static int lu_factor_blocks(int64_t B, int64_t N, float* A, int* piv, int* info, int* perm, int* sig, float* linv,
                             hipStream_t s, bool gather) {
   const bool vec = (N % 4 == 0) && aligned16(A);
   IADMM_ALLOW_LDS(lu_trail_kernel<true>, kTrailLds);
@@ -1509,35 +1585,49 @@ static int lu_factor_blocks(int64_t B, int64_t N, float* A, int* piv, int* info,
   IADMM_ALLOW_LDS(lu_trail_kernel<false>, kTrailLds);
   IADMM_ALLOW_LDS(lu_trail128_kernel<true>, kT2Lds);
   IADMM_ALLOW_LDS(lu_trail128_kernel<false>, kT2Lds);
+  // defer: the interchanges left of each block wait for one final pass (lu_left_*_kernel); every
+  // block keeps its permutation in a slot of its own until then
+  const bool defer = gather && N <= kLeftDeferMaxN;
+  const int nb = (int)((N + kOB - 1) / kOB);
+  const int64_t slot = B * (int64_t)kPermInts;
   int rc = 0;
   for (int P = 0; P < N && !rc; P += kOB) {
     const int n_ = (int)N;
     const int c1 = std::min(n_, P + kBlk), c2 = std::min(n_, P + kOB);
+    int* pm = defer ? perm + (P / kOB) * slot : perm;
     // first half: factor; its interchanges and U12 on the second half's columns only, then the second
     // half's rank-64 update
     rc = lu_factor_half(B, N, P, c1, A, piv, info, s);
-    if (!rc && c1 < n_) rc = lu_swap(B, N, P, c1, 0, 0, c1, c2, c2, A, piv, perm, s);
+    if (!rc && c1 < n_) rc = lu_swap(B, N, P, c1, 0, 0, c1, c2, c2, A, piv, pm, s);
     if (!rc) rc = lu_rank64(B, N, P, c1, c2, A, vec, s);
     // second half: factor; its interchanges on the first half's columns
     if (!rc && c1 < n_) rc = lu_factor_half(B, N, c1, c2, A, piv, info, s);
-    if (!rc && c1 < n_) rc = lu_swap(B, N, c1, c2, P, c1, 0, 0, 0, A, piv, perm, s);
-    // the whole block's interchanges composed into one row permutation: applied here to the columns
-    // left of the block, and inside lu_trail128_kernel (gathered loads) to the columns right of it --
-    // or here too (gather = false: N above the trailing kernel's LDS tables), then an
-    // interchange-free trailing update
+    if (!rc && c1 < n_) rc = lu_swap(B, N, c1, c2, P, c1, 0, 0, 0, A, piv, pm, s);
+    // the whole block's interchanges composed into one row permutation: applied to the columns right
+    // of the block inside lu_trail128_kernel (gathered loads) -- or here (gather = false: N above the
+    // trailing kernel's LDS tables), then an interchange-free trailing update -- and to the columns
+    // left of it here, or at the end (defer)
     if (rc) break;
-    hipLaunchKernelGGL(lu_block_perm_kernel, dim3((unsigned)B), dim3(64), 0, s, (int)N, P, c2, piv, perm);
+    hipLaunchKernelGGL(lu_block_perm_kernel, dim3((unsigned)B), dim3(64), 0, s, (int)N, P, c2, piv, pm);
     IADMM_CHECK_LAUNCH();
-    rc = lu_swap(B, N, P, c2, 0, P, gather ? 0 : c2, gather ? 0 : n_, 0, A, piv, perm, s, false);
+    rc = lu_swap(B, N, P, c2, 0, defer ? 0 : P, gather ? 0 : c2, gather ? 0 : n_, 0, A, piv, pm, s, false);
     if (rc || c2 >= n_) break;
     // U12 = L11^-1 A12 and the rank-128 update of everything right of the block
     hipLaunchKernelGGL(lu_linv_kernel, dim3((unsigned)B), dim3(kOB), 0, s, (int)N, P, A, linv);
     IADMM_CHECK_LAUNCH();
     const int ntc = ((int)N - c2 + kT2C - 1) / kT2C;
     const dim3 grid((unsigned)(B * ntc));
-    const int* gp = gather ? perm : nullptr;
+    const int* gp = gather ? pm : nullptr;
     if (vec) hipLaunchKernelGGL(lu_trail128_kernel<true>, grid, dim3(kT2Threads), kT2Lds, s, (int)N, P, ntc, A, linv, gp);
     else hipLaunchKernelGGL(lu_trail128_kernel<false>, grid, dim3(kT2Threads), kT2Lds, s, (int)N, P, ntc, A, linv, gp);
+    IADMM_CHECK_LAUNCH();
+  }
+  if (!rc && defer && nb > 1) {
+    hipLaunchKernelGGL(lu_left_compose_kernel, dim3((unsigned)B), dim3(64), 0, s, (int)N, nb, slot, perm, sig);
+    IADMM_CHECK_LAUNCH();
+    const dim3 grid((unsigned)(B * 4 * (nb - 1)));
+    if (vec) hipLaunchKernelGGL(lu_left_apply_kernel<true>, grid, dim3(1024), 0, s, (int)N, (int)B, sig, A);
+    else hipLaunchKernelGGL(lu_left_apply_kernel<false>, grid, dim3(1024), 0, s, (int)N, (int)B, sig, A);
     IADMM_CHECK_LAUNCH();
   }
   return rc;
@@ -1674,20 +1764,30 @@ static int lu_solve_hbm(int64_t B, int64_t N, const float* LU, const int* piv, f
   return 0;
 }
 
-// workspace: per-instance block permutations (kPermInts ints) + the 128 x 128 L11^-1 of the current
-// outer block (16-B aligned after the permutations)
-static int64_t lu_perm_bytes(int64_t B) { return ((B * (int64_t)kPermInts * (int64_t)sizeof(int)) + 15) / 16 * 16; }
-static int64_t lu_ws_bytes(int64_t B) { return lu_perm_bytes(B) + B * (int64_t)kLinvFloats * (int64_t)sizeof(float); }
+// workspace: per-instance block permutations (kPermInts ints; N <= kLeftDeferMaxN: one slot per
+// 128-column block, then the deferred left interchanges' sigma tables), then the 128 x 128 L11^-1 of
+// the current outer block (each part 16-B aligned)
+static int64_t al16(int64_t n) { return (n + 15) / 16 * 16; }
+static int64_t lu_nb(int64_t N) { return (N + kOB - 1) / kOB; }
+static int64_t lu_perm_bytes(int64_t B, int64_t N) {
+  return al16(B * (int64_t)kPermInts * (N <= kLeftDeferMaxN ? lu_nb(N) : 1) * (int64_t)sizeof(int));
+}
+static int64_t lu_sig_bytes(int64_t B, int64_t N) {
+  return N <= kLeftDeferMaxN ? al16(B * left_sig_off(N, lu_nb(N) - 1) * (int64_t)sizeof(int)) : 0;
+}
+static int64_t lu_ws_bytes(int64_t B, int64_t N) {
+  return lu_perm_bytes(B, N) + lu_sig_bytes(B, N) + B * (int64_t)kLinvFloats * (int64_t)sizeof(float);
+}
 
 extern "C" int64_t iadmm_lu_factor_ws_bytes(int64_t B, int64_t N) {
   if (B <= 0 || N <= 0) return 0;
-  return lu_ws_bytes(B);
+  return lu_ws_bytes(B, N);
 }
 
 extern "C" int iadmm_lu_factor(int64_t B, int64_t N, float* A, int* piv, int* info, void* ws, int64_t ws_bytes,
                                void* stream) {
   if (B <= 0 || N <= 0 || !A || !piv || !info || !ws) return IADMM_E_ARG;
-  if (ws_bytes < lu_ws_bytes(B)) return IADMM_E_ARG;
+  if (ws_bytes < lu_ws_bytes(B, N)) return IADMM_E_ARG;
   if (!aligned16(ws)) return IADMM_E_ALIGN;
   if (N > kLuMaxHbmN || B > 0x7fffffff) return IADMM_E_SIZE;
   const int64_t ntc_max = (N + kTC - 1) / kTC, nrc_max = (N + kTRW - 1) / kTRW;
@@ -1696,8 +1796,9 @@ extern "C" int iadmm_lu_factor(int64_t B, int64_t N, float* A, int* piv, int* in
   const hipError_t e = hipMemsetAsync(info, 0, B * sizeof(int), s);
   if (e != hipSuccess) return (int)e;
   int* perm = static_cast<int*>(ws);
-  float* linv = reinterpret_cast<float*>(static_cast<char*>(ws) + lu_perm_bytes(B));
-  return lu_factor_blocks(B, N, A, piv, info, perm, linv, s, N <= kLuMaxN && !lu_force_hbm());
+  int* sig = reinterpret_cast<int*>(static_cast<char*>(ws) + lu_perm_bytes(B, N));
+  float* linv = reinterpret_cast<float*>(static_cast<char*>(ws) + lu_perm_bytes(B, N) + lu_sig_bytes(B, N));
+  return lu_factor_blocks(B, N, A, piv, info, perm, sig, linv, s, N <= kLuMaxN && !lu_force_hbm());
 }
 
 extern "C" int iadmm_lu_solve(int64_t B, int64_t N, const float* LU, const int* piv, float* x,
