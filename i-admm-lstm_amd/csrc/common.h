@@ -182,3 +182,9 @@ __host__ __device__ inline bool aligned16(const void* p) { return (reinterpret_c
     hipError_t e_ = hipGetLastError();                \
     if (e_ != hipSuccess) return static_cast<int>(e_); \
   } while (0)
+
+#define IADMM_HIP_RC(call)                            \
+  do {                                                \
+    hipError_t e_ = (call);                           \
+    if (e_ != hipSuccess) return static_cast<int>(e_); \
+  } while (0)

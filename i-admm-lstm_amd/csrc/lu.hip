@@ -18,8 +18,11 @@
 // gathered loads and left of it at the end, all blocks in one pass (lu_left_compose_kernel +
 // lu_left_apply_kernel; N > 2048: per block, lu_swap_kernel<128, false>); L11^-1 (lu_linv_kernel); then
 //   lu_trail128_kernel     U12 = L11^-1 A12 (MFMA prologue) and A22 -= L21 U12 at rank 128 on fp32
-//                          MFMA (v_mfma_f32_32x32x2f32): 128-column strips streamed in 64-row
-//                          steps, A22 read + written once per 128 columns.
+//                          MFMA (v_mfma_f32_32x32x2f32): 128-column strips streamed in 32-row
+//                          steps, A22 read + written once per 128 columns.  With the left
+//                          interchanges deferred, strip 0 (the next block's columns) runs on the
+//                          caller's stream and the other strips on a side stream, beside the
+//                          next block's factorization (look-ahead, lu_factor_blocks).
 // lu_solve_kernel: one workgroup per instance; P b, then blocked forward (unit L) and backward
 // (U) substitution: 64-row blocks, prefix dot products over coalesced row segments, the 64x64
 // diagonal block solved inside one wave.
@@ -36,6 +39,7 @@
 // pivot (0 = non-singular), LAPACK convention.
 #include <algorithm>
 #include <cstdlib>
+#include <mutex>
 #include <type_traits>
 
 #include "common.h"
@@ -667,11 +671,14 @@ __global__ __launch_bounds__(64) void lu_block_perm_kernel(int N, int K0, int ce
 // an original block row, so: the new block rows are loaded first (x, registers), then the outside
 // rows are moved 16 at a time (their sources are block rows, which are only stored to afterwards),
 // then the substitution and the block-row stores.
-template <int NBK, bool TRSM>
+// BUILD (one workgroup per instance, r04): the permutation is built here from piv by wave 0
+// (build_row_perm) instead of read from perm -- no lu_block_perm_kernel launch in front.
+template <int NBK, bool TRSM, bool BUILD = false>
 __global__ __launch_bounds__(256) void lu_swap_kernel(int N, int K0, int nbk, int a0, int a1, int b0, int b1,
-                                                      int trsm_end, float* A, const int* perm) {
+                                                      int trsm_end, float* A, const int* perm, const int* piv) {
   __shared__ float Ld[TRSM ? kBlk : 1][kBlk + 1];
   __shared__ int prow[2 * kPermMax], pcur[2 * kPermMax], pcnt[1];
+  __shared__ int pvs[BUILD ? kPermMax : 1];
   const int tid = threadIdx.x;
   const size_t b = blockIdx.x;
   float* Ab = A + b * (size_t)N * N;
@@ -689,10 +696,16 @@ __global__ __launch_bounds__(256) void lu_swap_kernel(int N, int K0, int nbk, in
       Ld[idx / kBlk][idx % kBlk] = lv[q];
     }
   }
-  const int* pb = perm + b * kPermInts;
-  for (int i = tid; i < 2 * kPermMax; i += blockDim.x) { prow[i] = pb[i]; pcur[i] = pb[2 * kPermMax + i]; }
-  if (tid == 0) *pcnt = pb[4 * kPermMax];
-  __syncthreads();
+  if constexpr (BUILD) {
+    for (int i = tid; i < nbk; i += blockDim.x) pvs[i] = piv[b * N + K0 + i] - 1;
+    __syncthreads();
+    build_row_perm(pvs, K0, nbk, prow, pcur, pcnt);  // (ends with a barrier)
+  } else {
+    const int* pb = perm + b * kPermInts;
+    for (int i = tid; i < 2 * kPermMax; i += blockDim.x) { prow[i] = pb[i]; pcur[i] = pb[2 * kPermMax + i]; }
+    if (tid == 0) *pcnt = pb[4 * kPermMax];
+    __syncthreads();
+  }
   const int cnt = *pcnt;
   const int q = blockIdx.y * blockDim.x + tid, na = a1 - a0;
   const int c = q < na ? a0 + q : b0 + (q - na);
@@ -987,7 +1000,7 @@ __global__ __launch_bounds__(kOB) void lu_linv_kernel(int N, int P, const float*
 // Strips of one instance are consecutive logical ids on one XCD (its L2 serves the L21 re-reads).
 // DIAG (tools/lubench128.hip only): 1 = no MFMAs in the main loop, 2 = no global A22 / L21 traffic in it.
 template <bool VEC, int DIAG = 0>
-__global__ __launch_bounds__(kT2Threads, 2) void lu_trail128_kernel(int N, int P, int ntc, float* A,
+__global__ __launch_bounds__(kT2Threads, 2) void lu_trail128_kernel(int N, int P, int ntc, int tc0, float* A,
                                                                     const float* Linv, const int* perm) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   float* Ls0 = sm;                      // 2 x [kT2S rows][kT2K]: L21 of a step
@@ -1005,7 +1018,7 @@ __global__ __launch_bounds__(kT2Threads, 2) void lu_trail128_kernel(int N, int P
   const int xcd = bid & 7, local = bid >> 3, q8 = nwg >> 3, r8 = nwg & 7;
   const int logical = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + local;
   const size_t b = (size_t)(logical / ntc);
-  const int tc = logical % ntc;
+  const int tc = tc0 + logical % ntc;  // (this launch's strips: [tc0, tc0 + ntc))
   float* Ab = A + b * (size_t)N * N;
   const int c0 = P + kOB, cb = c0 + tc * kT2C;
   const int nsteps = (N - c0 + kT2S - 1) / kT2S;
@@ -1465,20 +1478,24 @@ __global__ __launch_bounds__(64) void lu_left_compose_kernel(int N, int nb, int6
   }
 }
 
-// rows [128 (j + 1), N) of a 32-column piece of block j take rows sigma_j (in place: every load of
-// the piece, then the workgroup's barrier, then every store).  Workgroup g: instance g % B, piece
-// (g / B) % 4 of block (g / B) / 4, the heavy blocks (small j) first.  VEC: 16-B accesses, 8 lanes
-// per row (a 128-B line per row and piece).
+// rows [128 (j + 1), N) of a 16-column piece of block j take rows sigma_j (in place: every load of
+// the piece, then the workgroup's barrier, then every store).  512 threads hold the piece in
+// registers (15 float4 each, 96 VGPRs: two workgroups per CU, 240 KB in flight); the eight
+// pieces of one (instance, block) are consecutive logical ids on one XCD, so the two 64-B halves of
+// each 128-B line meet in that XCD's L2.  (r04 first form: 32-column pieces on 1024 threads, one
+// workgroup per CU: 4.9 ms per factorization, ~3 TB/s.)  VEC: 16-B accesses.
 template <bool VEC>
-__global__ __launch_bounds__(1024) void lu_left_apply_kernel(int N, int B, const int* sig, float* A) {
-  constexpr int kLpr = VEC ? 8 : 32, kRpp = 1024 / kLpr;
+__global__ __launch_bounds__(512) void lu_left_apply_kernel(int N, int nb1, const int* sig, float* A) {
+  constexpr int kLpr = VEC ? 4 : 16, kRpp = 512 / kLpr;
   constexpr int kPass = (kLeftDeferMaxN - kOB + kRpp - 1) / kRpp;
   typedef typename std::conditional<VEC, float4v, float>::type T;
-  const int g = blockIdx.x, b = g % B, jq = g / B, j = jq >> 2;
+  const int g = blockIdx.x, q8 = gridDim.x >> 3;  // (gridDim.x = 8 pieces x B x nb1)
+  const int logical = (g & 7) * q8 + (g >> 3), piece = logical & 7, rest = logical >> 3;
+  const int b = rest / nb1, j = rest % nb1;
   const int tid = threadIdx.x, rr = tid / kLpr;
-  const int c = kOB * j + 32 * (jq & 3) + (VEC ? 4 : 1) * (tid % kLpr);
+  const int c = kOB * j + 16 * piece + (VEC ? 4 : 1) * (tid % kLpr);
   const int r0 = kOB * (j + 1), R = N - r0;
-  const int* sg = sig + (size_t)b * left_sig_off(N, (N + kOB - 1) / kOB - 1) + left_sig_off(N, j);
+  const int* sg = sig + (size_t)b * left_sig_off(N, nb1) + left_sig_off(N, j);
   float* Ab = A + (size_t)b * N * N;
   T v[kPass];
 #pragma unroll
@@ -1548,17 +1565,25 @@ static int lu_swap(int64_t B, int64_t N, int K0, int cend, int a0, int a1, int b
   b1 = std::max(b0, b1);
   const int cols = (a1 - a0) + (b1 - b0), nbk = cend - K0;
   if (cols <= 0 || nbk <= 0) return 0;
+  const dim3 grid((unsigned)B, (unsigned)((cols + 255) / 256));
+  if (build && grid.y == 1 && nbk <= kBlk) {  // one workgroup per instance: built in the kernel
+    if (trsm_end > b0)
+      hipLaunchKernelGGL((lu_swap_kernel<kBlk, true, true>), grid, dim3(256), 0, s, (int)N, K0, nbk, a0, a1, b0, b1, trsm_end, A, perm, piv);
+    else
+      hipLaunchKernelGGL((lu_swap_kernel<kBlk, false, true>), grid, dim3(256), 0, s, (int)N, K0, nbk, a0, a1, b0, b1, 0, A, perm, piv);
+    IADMM_CHECK_LAUNCH();
+    return 0;
+  }
   if (build) {
     hipLaunchKernelGGL(lu_block_perm_kernel, dim3((unsigned)B), dim3(64), 0, s, (int)N, K0, cend, piv, perm);
     IADMM_CHECK_LAUNCH();
   }
-  const dim3 grid((unsigned)B, (unsigned)((cols + 255) / 256));
   if (trsm_end > b0)
-    hipLaunchKernelGGL((lu_swap_kernel<kBlk, true>), grid, dim3(256), 0, s, (int)N, K0, nbk, a0, a1, b0, b1, trsm_end, A, perm);
+    hipLaunchKernelGGL((lu_swap_kernel<kBlk, true>), grid, dim3(256), 0, s, (int)N, K0, nbk, a0, a1, b0, b1, trsm_end, A, perm, piv);
   else if (nbk <= kBlk)
-    hipLaunchKernelGGL((lu_swap_kernel<kBlk, false>), grid, dim3(256), 0, s, (int)N, K0, nbk, a0, a1, b0, b1, 0, A, perm);
+    hipLaunchKernelGGL((lu_swap_kernel<kBlk, false>), grid, dim3(256), 0, s, (int)N, K0, nbk, a0, a1, b0, b1, 0, A, perm, piv);
   else
-    hipLaunchKernelGGL((lu_swap_kernel<kPermMax, false>), grid, dim3(256), 0, s, (int)N, K0, nbk, a0, a1, b0, b1, 0, A, perm);
+    hipLaunchKernelGGL((lu_swap_kernel<kPermMax, false>), grid, dim3(256), 0, s, (int)N, K0, nbk, a0, a1, b0, b1, 0, A, perm, piv);
   IADMM_CHECK_LAUNCH();
   return 0;
 }
@@ -1577,6 +1602,36 @@ static int lu_rank64(int64_t B, int64_t N, int K0, int cend, int cmax, float* A,
   return 0;
 }
 
+// The look-ahead's side stream and its two events, per device, made on first use (non-blocking: no
+// implicit synchronisation with the null stream); the mutex keeps one factorization at a time on them.
+struct LuSide {
+  std::mutex mu;
+  hipStream_t s2 = nullptr;
+  hipEvent_t fork = nullptr, join = nullptr;
+};
+static LuSide* lu_side() {
+  static std::mutex mk;
+  static LuSide side[64];
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+  std::lock_guard<std::mutex> g(mk);
+  LuSide& d = side[dev];
+  if (!d.s2) {
+    hipStream_t st = nullptr;
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) return nullptr;
+    if (hipEventCreateWithFlags(&e0, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&e1, hipEventDisableTiming) != hipSuccess) {
+      (void)hipStreamDestroy(st);
+      return nullptr;
+    }
+    d.fork = e0;
+    d.join = e1;
+    d.s2 = st;
+  }
+  return &d;
+}
+
 static int lu_factor_blocks(int64_t B, int64_t N, float* A, int* piv, int* info, int* perm, int* sig, float* linv,
                             hipStream_t s, bool gather) {
   const bool vec = (N % 4 == 0) && aligned16(A);
@@ -1590,6 +1645,15 @@ static int lu_factor_blocks(int64_t B, int64_t N, float* A, int* piv, int* info,
   const bool defer = gather && N <= kLeftDeferMaxN;
   const int nb = (int)((N + kOB - 1) / kOB);
   const int64_t slot = B * (int64_t)kPermInts;
+  // look-ahead (with defer): block t's trailing update is two launches -- strip 0 (block t + 1's own
+  // columns) on s, the other strips on a side stream -- so that block t + 1's panels, interchanges,
+  // in-block updates and L11^-1, which touch only block t + 1's columns once the left interchanges
+  // are deferred, run beside the rest of block t's update; block t + 1's trailing update waits for
+  // it.  L11^-1 alternates between two buffers (the side launch of block t still reads its own).
+  LuSide* side = defer ? lu_side() : nullptr;
+  std::unique_lock<std::mutex> side_lock;
+  if (side) side_lock = std::unique_lock<std::mutex>(side->mu);
+  bool pending = false;  // a side launch not yet joined
   int rc = 0;
   for (int P = 0; P < N && !rc; P += kOB) {
     const int n_ = (int)N;
@@ -1613,21 +1677,44 @@ static int lu_factor_blocks(int64_t B, int64_t N, float* A, int* piv, int* info,
     rc = lu_swap(B, N, P, c2, 0, defer ? 0 : P, gather ? 0 : c2, gather ? 0 : n_, 0, A, piv, pm, s, false);
     if (rc || c2 >= n_) break;
     // U12 = L11^-1 A12 and the rank-128 update of everything right of the block
-    hipLaunchKernelGGL(lu_linv_kernel, dim3((unsigned)B), dim3(kOB), 0, s, (int)N, P, A, linv);
+    float* lv = linv + (side ? ((P / kOB) & 1) * B * (int64_t)kLinvFloats : 0);
+    hipLaunchKernelGGL(lu_linv_kernel, dim3((unsigned)B), dim3(kOB), 0, s, (int)N, P, A, lv);
     IADMM_CHECK_LAUNCH();
     const int ntc = ((int)N - c2 + kT2C - 1) / kT2C;
-    const dim3 grid((unsigned)(B * ntc));
     const int* gp = gather ? pm : nullptr;
-    if (vec) hipLaunchKernelGGL(lu_trail128_kernel<true>, grid, dim3(kT2Threads), kT2Lds, s, (int)N, P, ntc, A, linv, gp);
-    else hipLaunchKernelGGL(lu_trail128_kernel<false>, grid, dim3(kT2Threads), kT2Lds, s, (int)N, P, ntc, A, linv, gp);
+    auto trail = [&](hipStream_t st, int tc0, int cnt) {
+      const dim3 grid((unsigned)(B * cnt));
+      if (vec) hipLaunchKernelGGL(lu_trail128_kernel<true>, grid, dim3(kT2Threads), kT2Lds, st, (int)N, P, cnt, tc0, A, lv, gp);
+      else hipLaunchKernelGGL(lu_trail128_kernel<false>, grid, dim3(kT2Threads), kT2Lds, st, (int)N, P, cnt, tc0, A, lv, gp);
+    };
+    if (!side) {
+      trail(s, 0, ntc);
+      IADMM_CHECK_LAUNCH();
+      continue;
+    }
+    if (pending) IADMM_HIP_RC(hipStreamWaitEvent(s, side->join, 0));  // block t - 1's other strips
+    pending = false;
+    if (ntc > 1) {
+      IADMM_HIP_RC(hipEventRecord(side->fork, s));
+      IADMM_HIP_RC(hipStreamWaitEvent(side->s2, side->fork, 0));
+      trail(side->s2, 1, ntc - 1);
+      IADMM_CHECK_LAUNCH();
+      IADMM_HIP_RC(hipEventRecord(side->join, side->s2));
+      pending = true;
+    }
+    trail(s, 0, 1);
     IADMM_CHECK_LAUNCH();
+  }
+  if (pending) {
+    const hipError_t e = hipStreamWaitEvent(s, side->join, 0);
+    if (e != hipSuccess && !rc) rc = (int)e;
   }
   if (!rc && defer && nb > 1) {
     hipLaunchKernelGGL(lu_left_compose_kernel, dim3((unsigned)B), dim3(64), 0, s, (int)N, nb, slot, perm, sig);
     IADMM_CHECK_LAUNCH();
-    const dim3 grid((unsigned)(B * 4 * (nb - 1)));
-    if (vec) hipLaunchKernelGGL(lu_left_apply_kernel<true>, grid, dim3(1024), 0, s, (int)N, (int)B, sig, A);
-    else hipLaunchKernelGGL(lu_left_apply_kernel<false>, grid, dim3(1024), 0, s, (int)N, (int)B, sig, A);
+    const dim3 grid((unsigned)(B * 8 * (nb - 1)));
+    if (vec) hipLaunchKernelGGL(lu_left_apply_kernel<true>, grid, dim3(512), 0, s, (int)N, nb - 1, sig, A);
+    else hipLaunchKernelGGL(lu_left_apply_kernel<false>, grid, dim3(512), 0, s, (int)N, nb - 1, sig, A);
     IADMM_CHECK_LAUNCH();
   }
   return rc;
@@ -1775,8 +1862,9 @@ static int64_t lu_perm_bytes(int64_t B, int64_t N) {
 static int64_t lu_sig_bytes(int64_t B, int64_t N) {
   return N <= kLeftDeferMaxN ? al16(B * left_sig_off(N, lu_nb(N) - 1) * (int64_t)sizeof(int)) : 0;
 }
-static int64_t lu_ws_bytes(int64_t B, int64_t N) {
-  return lu_perm_bytes(B, N) + lu_sig_bytes(B, N) + B * (int64_t)kLinvFloats * (int64_t)sizeof(float);
+static int64_t lu_ws_bytes(int64_t B, int64_t N) {  // (two L11^-1 buffers with the look-ahead)
+  return lu_perm_bytes(B, N) + lu_sig_bytes(B, N) +
+         (N <= kLeftDeferMaxN ? 2 : 1) * B * (int64_t)kLinvFloats * (int64_t)sizeof(float);
 }
 
 extern "C" int64_t iadmm_lu_factor_ws_bytes(int64_t B, int64_t N) {

@@ -596,7 +596,7 @@ template <int WS, int DIAG>
 void launch(int B, int N, int P, float* A, float* Linv) {
   const int ntc = (N - P - kOB + kT2C - 1) / kT2C;
   if (WS == 2) hipLaunchKernelGGL((lu_trail128d_kernel<DIAG>), dim3(B * ntc), dim3(256), kDLds, 0, N, P, ntc, A, Linv, nullptr);
-  else if (WS) hipLaunchKernelGGL((lu_trail128_kernel<true, DIAG>), dim3(B * ntc), dim3(kT2Threads), kT2Lds, 0, N, P, ntc, A, Linv, nullptr);
+  else if (WS) hipLaunchKernelGGL((lu_trail128_kernel<true, DIAG>), dim3(B * ntc), dim3(kT2Threads), kT2Lds, 0, N, P, ntc, 0, A, Linv, nullptr);
   else hipLaunchKernelGGL((lu_trail128_r03_kernel<true, DIAG>), dim3(B * ntc), dim3(kR3Threads), kR3Lds, 0, N, P, ntc, A, Linv, nullptr);
 }
 
