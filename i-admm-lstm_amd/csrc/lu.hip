@@ -109,9 +109,14 @@ constexpr int kTC = 128;          // trailing update: columns per workgroup stri
 constexpr int kTRS = 64;          //   rows per pipeline step
 constexpr int kTRW = 1024;        //   rows per workgroup
 constexpr int kTS = kBlk + 4;     //   LDS row stride of the staged U12^T / -L21 blocks
-constexpr int kCS = kTC + 8;      //   LDS row stride of the A22 staging tiles (conflict-free acc access)
 constexpr int kTrailThreads = 512;
-constexpr size_t kTrailLds = ((kTC + 2 * kTRS) * kTS + 2 * kTRS * kCS) * sizeof(float);
+// LDS of lu_trail_kernel<.., TCW>: U12^T [TCW][kTS], -L21 [kTRS][kTS] (one buffer: it is rewritten
+// only after the step's barrier), Cin / Cout [kTRS][TCW + 8].  TCW = 64 (the mid update): 70 KB, so
+// under the look-ahead it fits on a CU beside one lu_trail128_kernel workgroup (r04; the r03 layout,
+// 136 KB for any TCW, waited for whole CUs to drain).
+template <int TCW>
+constexpr size_t trail_lds() { return ((size_t)(TCW + kTRS) * kTS + 2 * (size_t)kTRS * (TCW + 8)) * sizeof(float); }
+constexpr size_t kTrailLds = trail_lds<kTC>();
 
 // The net row permutation of n interchanges (row base + j <-> pv[j], in order, ?laswp):
 // afterwards row rowid[i] holds what row cur[i] held before, for i < *cnt (<= 2n <= 256; rowid[i] =
@@ -746,7 +751,7 @@ __global__ __launch_bounds__(256) void lu_swap_kernel(int N, int K0, int nbk, in
 // one-step software pipeline.  A22 moves between HBM and the accumulators through LDS (Cin /
 // Cout) so that the global accesses are row-contiguous 16-B lanes (512 B per row per half-wave:
 // the MFMA layout's own 2-rows-x-128-B dword pattern ran at a third of that rate); -L21 is
-// double-buffered in LDS (Ls).  Wave (wr, wc) owns 32 x 32 of a step = one
+// staged in LDS (Ls).  Wave (wr, wc) owns 32 x 32 of a step = one
 // v_mfma_f32_32x32x2f32 accumulator; both operands are 16-B LDS reads along k: lane half h covers
 // k in [32h, 32h + 32) and MFMA step s uses k = 32h + s (any k order gives the same sum set).  The
 // strips of one instance are consecutive logical ids on one XCD (its L2 serves the -L21 re-reads
@@ -759,10 +764,11 @@ template <bool VEC, int DIAG = 0, int TCW = kTC>
 __global__ __launch_bounds__(kTrailThreads, 1) void lu_trail_kernel(int N, int K0, int ntc, int nrc, int cmax,
                                                                       float* A) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
-  float* Ut = sm;                       // [kTC cols][kTS]: U12^T
-  float* Lsb = Ut + kTC * kTS;          // 2 x [kTRS rows][kTS]: -L21
-  float* Cin = Lsb + 2 * kTRS * kTS;    // [kTRS rows][kCS]: next step's A22 rows
-  float* Cout = Cin + kTRS * kCS;       // [kTRS rows][kCS]: this step's result rows
+  constexpr int kCSw = TCW + 8;         // A22 tile stride (8 mod 32 banks: conflict-free acc access)
+  float* Ut = sm;                       // [TCW cols][kTS]: U12^T
+  float* Lsb = Ut + TCW * kTS;          // [kTRS rows][kTS]: -L21
+  float* Cin = Lsb + kTRS * kTS;        // [kTRS rows][kCSw]: next step's A22 rows
+  float* Cout = Cin + kTRS * kCSw;      // [kTRS rows][kCSw]: this step's result rows
   const int nwg = gridDim.x, bid = blockIdx.x;
   const int xcd = bid & 7, local = bid >> 3, q8 = nwg >> 3, r8 = nwg & 7;
   const int logical = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + local;
@@ -815,14 +821,14 @@ __global__ __launch_bounds__(kTrailThreads, 1) void lu_trail_kernel(int N, int K
 #pragma unroll
     for (int q = 0; q < kCQ; ++q) {
       const int e = tid + NT * q;
-      st_lds(Cin + (e / CPR) * kCS + (e % CPR) * W, c[q], 1.f);
+      st_lds(Cin + (e / CPR) * kCSw + (e % CPR) * W, c[q], 1.f);
     }
   };
-  auto writeL = [&](int buf, const VT (&l)[kLQ]) {
+  auto writeL = [&](const VT (&l)[kLQ]) {
 #pragma unroll
     for (int q = 0; q < kLQ; ++q) {
       const int e = tid + NT * q;
-      st_lds(Lsb + buf * kTRS * kTS + (e / LPR) * kTS + (e % LPR) * W, l[q], -1.f);
+      st_lds(Lsb + (e / LPR) * kTS + (e % LPR) * W, l[q], -1.f);
     }
   };
   auto storeOut = [&](int step) {
@@ -830,20 +836,24 @@ __global__ __launch_bounds__(kTrailThreads, 1) void lu_trail_kernel(int N, int K
     for (int q = 0; q < kCQ; ++q) {
       const int e = tid + NT * q, row = rs + step * kTRS + e / CPR, col = cb + (e % CPR) * W;
       if (row < re && col < cmax) {
-        const float* s = Cout + (e / CPR) * kCS + (e % CPR) * W;
+        const float* s = Cout + (e / CPR) * kCSw + (e % CPR) * W;
         if constexpr (VEC) *reinterpret_cast<float4*>(Ab + (size_t)row * N + col) = *reinterpret_cast<const float4*>(s);
         else Ab[(size_t)row * N + col] = *s;
       }
     }
   };
-  // accumulator register v <-> tile row wr + 8(v/4) + 4h + v%4, column wc + il
+  // accumulator register v <-> tile row wr + 8(v/4) + 4h + v%4, column wc + il (waves of columns
+  // >= TCW have no tile)
+  const bool tile = TCW == kTC || wc < TCW;
   auto accFromCin = [&](floatx16& acc) {
+    if (!tile) return;
 #pragma unroll
-    for (int v = 0; v < 16; ++v) acc[v] = Cin[(wr + 8 * (v >> 2) + 4 * h + (v & 3)) * kCS + wc + il];
+    for (int v = 0; v < 16; ++v) acc[v] = Cin[(wr + 8 * (v >> 2) + 4 * h + (v & 3)) * kCSw + wc + il];
   };
   auto accToCout = [&](const floatx16& acc) {
+    if (!tile) return;
 #pragma unroll
-    for (int v = 0; v < 16; ++v) Cout[(wr + 8 * (v >> 2) + 4 * h + (v & 3)) * kCS + wc + il] = acc[v];
+    for (int v = 0; v < 16; ++v) Cout[(wr + 8 * (v >> 2) + 4 * h + (v & 3)) * kCSw + wc + il] = acc[v];
   };
 
   VT cr[kCQ], lr[kLQ];
@@ -861,9 +871,9 @@ __global__ __launch_bounds__(kTrailThreads, 1) void lu_trail_kernel(int N, int K
     }
   }
   writeC(cr);
-  writeL(0, lr);
+  writeL(lr);
   __syncthreads();
-  floatx16 acc;
+  floatx16 acc = {};
   accFromCin(acc);
 
   for (int step = 0; step < nsteps; ++step) {
@@ -872,8 +882,8 @@ __global__ __launch_bounds__(kTrailThreads, 1) void lu_trail_kernel(int N, int K
       loadC(step + 1, cr);
       loadL(step + 1, lr);
     }
-    if (DIAG != 1 && (TCW == kTC || wc < TCW)) {
-      const float* Ls = Lsb + (step & 1) * kTRS * kTS;
+    if (DIAG != 1 && tile) {
+      const float* Ls = Lsb;
 #pragma unroll
       for (int sg = 0; sg < 8; ++sg) {
         const float4 fa = *reinterpret_cast<const float4*>(Ls + (wr + il) * kTS + 32 * h + 4 * sg);
@@ -883,10 +893,10 @@ __global__ __launch_bounds__(kTrailThreads, 1) void lu_trail_kernel(int N, int K
       }
     }
     accToCout(acc);
-    __syncthreads();  // Cin (this step's rows) and Ls[step & 1] fully consumed, Cout complete
+    __syncthreads();  // Cin (this step's rows) and Ls fully consumed, Cout complete
     if (more) {
       writeC(cr);
-      writeL((step + 1) & 1, lr);
+      writeL(lr);
     }
     storeOut(step);
     __syncthreads();  // Cout drained, Cin / Ls hold the next step
@@ -1595,7 +1605,7 @@ static int lu_rank64(int64_t B, int64_t N, int K0, int cend, int cmax, float* A,
   const int ntc = (wid + kTC - 1) / kTC, nrc = (rest + kTRW - 1) / kTRW;
   const dim3 grid((unsigned)(B * ntc * nrc));
   if (vec && wid <= kTC / 2)
-    hipLaunchKernelGGL((lu_trail_kernel<true, 0, kTC / 2>), grid, dim3(kTrailThreads), kTrailLds, s, (int)N, K0, ntc, nrc, cmax, A);
+    hipLaunchKernelGGL((lu_trail_kernel<true, 0, kTC / 2>), grid, dim3(kTrailThreads), trail_lds<kTC / 2>(), s, (int)N, K0, ntc, nrc, cmax, A);
   else if (vec) hipLaunchKernelGGL(lu_trail_kernel<true>, grid, dim3(kTrailThreads), kTrailLds, s, (int)N, K0, ntc, nrc, cmax, A);
   else hipLaunchKernelGGL(lu_trail_kernel<false>, grid, dim3(kTrailThreads), kTrailLds, s, (int)N, K0, ntc, nrc, cmax, A);
   IADMM_CHECK_LAUNCH();
@@ -1636,7 +1646,7 @@ static int lu_factor_blocks(int64_t B, int64_t N, float* A, int* piv, int* info,
                             hipStream_t s, bool gather) {
   const bool vec = (N % 4 == 0) && aligned16(A);
   IADMM_ALLOW_LDS(lu_trail_kernel<true>, kTrailLds);
-  IADMM_ALLOW_LDS((lu_trail_kernel<true, 0, kTC / 2>), kTrailLds);
+  IADMM_ALLOW_LDS((lu_trail_kernel<true, 0, kTC / 2>), trail_lds<kTC / 2>());
   IADMM_ALLOW_LDS(lu_trail_kernel<false>, kTrailLds);
   IADMM_ALLOW_LDS(lu_trail128_kernel<true>, kT2Lds);
   IADMM_ALLOW_LDS(lu_trail128_kernel<false>, kT2Lds);
