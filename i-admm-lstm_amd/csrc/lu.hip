@@ -1612,12 +1612,16 @@ static int lu_rank64(int64_t B, int64_t N, int K0, int cend, int cmax, float* A,
   return 0;
 }
 
-// The look-ahead's side stream and its two events, per device, made on first use (non-blocking: no
-// implicit synchronisation with the null stream); the mutex keeps one factorization at a time on them.
+// The look-ahead's streams and events, per device, made on first use (non-blocking: no implicit
+// synchronisation with the null stream); the mutex keeps one factorization at a time on them.  s1
+// (the device's highest priority) carries the critical path -- the block factorizations and the
+// strips the next block needs -- and s2 (lowest) the rest of each trailing update, so that CUs
+// freed by s2's workgroups go to s1's first.  The caller's stream forks into s1 and joins it at
+// the end.
 struct LuSide {
   std::mutex mu;
-  hipStream_t s2 = nullptr;
-  hipEvent_t fork = nullptr, join = nullptr;
+  hipStream_t s1 = nullptr, s2 = nullptr;
+  hipEvent_t fork = nullptr, join = nullptr, ev0 = nullptr, ev1 = nullptr;
 };
 static LuSide* lu_side() {
   static std::mutex mk;
@@ -1627,23 +1631,35 @@ static LuSide* lu_side() {
   std::lock_guard<std::mutex> g(mk);
   LuSide& d = side[dev];
   if (!d.s2) {
-    hipStream_t st = nullptr;
-    hipEvent_t e0 = nullptr, e1 = nullptr;
-    if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) return nullptr;
-    if (hipEventCreateWithFlags(&e0, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&e1, hipEventDisableTiming) != hipSuccess) {
-      (void)hipStreamDestroy(st);
+    int least = 0, greatest = 0;
+    if (hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess) least = greatest = 0;
+    hipStream_t a = nullptr, c = nullptr;
+    hipEvent_t e[4] = {};
+    if (hipStreamCreateWithPriority(&a, hipStreamNonBlocking, greatest) != hipSuccess) return nullptr;
+    if (hipStreamCreateWithPriority(&c, hipStreamNonBlocking, least) != hipSuccess) {
+      (void)hipStreamDestroy(a);
       return nullptr;
     }
-    d.fork = e0;
-    d.join = e1;
-    d.s2 = st;
+    for (int i = 0; i < 4; ++i)
+      if (hipEventCreateWithFlags(&e[i], hipEventDisableTiming) != hipSuccess) {
+        for (int k = 0; k < i; ++k) (void)hipEventDestroy(e[k]);
+        (void)hipStreamDestroy(a);
+        (void)hipStreamDestroy(c);
+        return nullptr;
+      }
+    d.fork = e[0];
+    d.join = e[1];
+    d.ev0 = e[2];
+    d.ev1 = e[3];
+    d.s1 = a;
+    d.s2 = c;
   }
   return &d;
 }
 
 static int lu_factor_blocks(int64_t B, int64_t N, float* A, int* piv, int* info, int* perm, int* sig, float* linv,
-                            hipStream_t s, bool gather) {
+                            hipStream_t s0, bool gather) {
+  hipStream_t s = s0;
   const bool vec = (N % 4 == 0) && aligned16(A);
   IADMM_ALLOW_LDS(lu_trail_kernel<true>, kTrailLds);
   IADMM_ALLOW_LDS((lu_trail_kernel<true, 0, kTC / 2>), trail_lds<kTC / 2>());
@@ -1662,7 +1678,12 @@ static int lu_factor_blocks(int64_t B, int64_t N, float* A, int* piv, int* info,
   // it.  L11^-1 alternates between two buffers (the side launch of block t still reads its own).
   LuSide* side = defer ? lu_side() : nullptr;
   std::unique_lock<std::mutex> side_lock;
-  if (side) side_lock = std::unique_lock<std::mutex>(side->mu);
+  if (side) {
+    side_lock = std::unique_lock<std::mutex>(side->mu);
+    IADMM_HIP_RC(hipEventRecord(side->ev0, s0));
+    IADMM_HIP_RC(hipStreamWaitEvent(side->s1, side->ev0, 0));
+    s = side->s1;
+  }
   bool pending = false;  // a side launch not yet joined
   int rc = 0;
   for (int P = 0; P < N && !rc; P += kOB) {
@@ -1726,6 +1747,11 @@ static int lu_factor_blocks(int64_t B, int64_t N, float* A, int* piv, int* info,
     if (vec) hipLaunchKernelGGL(lu_left_apply_kernel<true>, grid, dim3(512), 0, s, (int)N, nb - 1, sig, A);
     else hipLaunchKernelGGL(lu_left_apply_kernel<false>, grid, dim3(512), 0, s, (int)N, nb - 1, sig, A);
     IADMM_CHECK_LAUNCH();
+  }
+  if (side) {  // the caller's stream joins s1 (which has joined s2)
+    const hipError_t e1 = hipEventRecord(side->ev1, s);
+    const hipError_t e2 = e1 == hipSuccess ? hipStreamWaitEvent(s0, side->ev1, 0) : e1;
+    if (e2 != hipSuccess && !rc) rc = (int)e2;
   }
   return rc;
 }
