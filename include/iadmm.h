@@ -114,8 +114,13 @@ int iadmm_kkt_rhs(int64_t B, int64_t n, int64_t m, int64_t num_ineq, const float
  * panels up to N = 2048, 8-column panels on 1024-thread workgroups above, held in registers up to 10240 panel
  * rows and in HBM beyond; rank-128 MFMA trailing update with the block's interchanges as gathered loads up to
  * N = 36736, as a pass of their own above; limit N <= 46340, N * N < 2^31).
+ * N <= 2048 (r04): the interchanges left of each block are applied once at the end, and the next block is
+ * factored beside the rest of each trailing update (look-ahead) on two library-owned streams of the current
+ * device (made once; high / low priority), forked from and joined back into `stream` -- the call stays
+ * asynchronous and ordered on `stream`.
  * ws: caller-owned, 16-B aligned device workspace of at least iadmm_lu_factor_ws_bytes(B, N) bytes
- * (per-instance block permutations and the 128x128 L11^-1 blocks); nothing is allocated inside. */
+ * (per-instance block permutations -- one per 128-column block for N <= 2048, with the composed
+ * left permutations -- and the 128x128 L11^-1 blocks, two for N <= 2048); nothing is allocated inside. */
 int64_t iadmm_lu_factor_ws_bytes(int64_t B, int64_t N);
 int iadmm_lu_factor(int64_t B, int64_t N, float* A, int* piv, int* info, void* ws, int64_t ws_bytes,
                     void* stream);
