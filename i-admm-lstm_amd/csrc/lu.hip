@@ -125,9 +125,11 @@ constexpr size_t kTrailLds = trail_lds<kTC>();
 // no LDS round trip (r04: the LDS-resident lists cost ~500 cycles per interchange, ~30 us for a
 // 128-row block); the lists go to LDS once at the end.  The caller moves each column with all loads
 // before all stores, one memory latency instead of n.
-IADMM_DEV void build_row_perm(const int* pv, int base, int n, int* rowid, int* cur, int* cnt) {
+// (wave: the wave that builds; sync = false: no closing barrier -- only that wave reads the lists)
+IADMM_DEV void build_row_perm(const int* pv, int base, int n, int* rowid, int* cur, int* cnt, int wave = 0,
+                              bool sync = true) {
   const int lane = threadIdx.x & 63;
-  if ((threadIdx.x >> 6) == 0) {
+  if ((int)(threadIdx.x >> 6) == wave) {
     int rw[4], cr[4];
 #pragma unroll
     for (int s = 0; s < 4; ++s) rw[s] = cr[s] = base + 64 * s + lane;
@@ -165,7 +167,7 @@ IADMM_DEV void build_row_perm(const int* pv, int base, int n, int* rowid, int* c
       if (64 * s + lane < c) { rowid[64 * s + lane] = rw[s]; cur[64 * s + lane] = cr[s]; }
     if (lane == 0) *cnt = c;
   }
-  __syncthreads();
+  if (sync) __syncthreads();
 }
 
 // The (N-k0) x 16 panel lives in registers: thread t owns rows t + 256 m (m < M), 16 columns
@@ -940,11 +942,27 @@ constexpr int kLinvFloats = kOB * kOB;
 // column in registers (both loops unrolled) and L broadcast from LDS 4 entries per read; four
 // partial sums per row shorten the dependent chains.  (r03 first form: L and X both in LDS, one
 // workgroup per CU, LDS-latency bound: 1.6 ms per block at B = 1024, 15x this one.)
-__global__ __launch_bounds__(kOB) void lu_linv_kernel(int N, int P, const float* A, float* Linv) {
+// perm != nullptr (r04, look-ahead): a third wave builds the block's composed permutation (what
+// lu_block_perm_kernel does) beside the substitution, one launch less on the critical path.
+__global__ __launch_bounds__(kOB + 64) void lu_linv_kernel(int N, int P, const float* A, float* Linv, const int* piv,
+                                                         int* perm, int cend) {
   __shared__ __attribute__((aligned(16))) float L[kOB][kOB + 4];
+  __shared__ int pvs[kPermMax], prow[2 * kPermMax], pcur[2 * kPermMax], pcnt[1];
   const int j = threadIdx.x;
   const size_t b = blockIdx.x;
   const float* Ab = A + b * (size_t)N * N;
+  if (j >= kOB) {  // the permutation wave
+    const int nbk = cend - P, lane = j - kOB;
+    if (perm)
+      for (int i = lane; i < nbk; i += 64) pvs[i] = piv[b * N + P + i] - 1;
+    __syncthreads();  // (the block's one barrier: L staged)
+    if (!perm) return;
+    build_row_perm(pvs, P, nbk, prow, pcur, pcnt, kOB / 64, false);
+    int* out = perm + b * kPermInts;
+    for (int i = lane; i < 2 * kPermMax; i += 64) { out[i] = prow[i]; out[2 * kPermMax + i] = pcur[i]; }
+    if (lane == 0) out[4 * kPermMax] = *pcnt;
+    return;
+  }
   // the 128 x 128 block in four batches of 32 row loads per thread (a batch's loads all in flight
   // together; r03 first form: a 128-iteration load -> LDS-store loop, one latency after another)
   constexpr int kLB = 32;
@@ -1703,13 +1721,18 @@ static int lu_factor_blocks(int64_t B, int64_t N, float* A, int* piv, int* info,
     // trailing kernel's LDS tables), then an interchange-free trailing update -- and to the columns
     // left of it here, or at the end (defer)
     if (rc) break;
-    hipLaunchKernelGGL(lu_block_perm_kernel, dim3((unsigned)B), dim3(64), 0, s, (int)N, P, c2, piv, pm);
-    IADMM_CHECK_LAUNCH();
+    // (defer: nothing to swap here, and L11^-1's kernel builds the permutation beside the substitution)
+    const bool perm_in_linv = defer && c2 < n_;
+    if (!perm_in_linv) {
+      hipLaunchKernelGGL(lu_block_perm_kernel, dim3((unsigned)B), dim3(64), 0, s, (int)N, P, c2, piv, pm);
+      IADMM_CHECK_LAUNCH();
+    }
     rc = lu_swap(B, N, P, c2, 0, defer ? 0 : P, gather ? 0 : c2, gather ? 0 : n_, 0, A, piv, pm, s, false);
     if (rc || c2 >= n_) break;
     // U12 = L11^-1 A12 and the rank-128 update of everything right of the block
     float* lv = linv + (side ? ((P / kOB) & 1) * B * (int64_t)kLinvFloats : 0);
-    hipLaunchKernelGGL(lu_linv_kernel, dim3((unsigned)B), dim3(kOB), 0, s, (int)N, P, A, lv);
+    hipLaunchKernelGGL(lu_linv_kernel, dim3((unsigned)B), dim3(kOB + 64), 0, s, (int)N, P, A, lv, piv,
+                       perm_in_linv ? pm : nullptr, c2);
     IADMM_CHECK_LAUNCH();
     const int ntc = ((int)N - c2 + kT2C - 1) / kT2C;
     const int* gp = gather ? pm : nullptr;
