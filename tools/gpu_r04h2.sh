@@ -1,16 +1,14 @@
 #!/bin/bash
-# r04 session 8, final HEAD: the whole -m gpu suite in one process, smoke, then the default bench
-# line (as the driver runs them)
+# r04 session 8: the default bench line at the final HEAD (as the driver runs it), after the K = 100
+# parity tests with the final checkpoint
 set -o pipefail
 mkdir -p gpurun_out
-bash tools/gpu_suite.sh r04i || exit $?
-timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/r04i_smoke.log 2>&1 || exit $?
-tail -1 gpurun_out/r04i_smoke.log
-timeout -k 10 900 python -u bench.py > gpurun_out/r04i_bench.log 2>&1 || exit $?
-grep '^{' gpurun_out/r04i_bench.log > gpurun_out/r04i_bench.json
+bash tools/gpu_tests.sh r04h2 600 tests/test_k100_gpu.py || exit $?
+timeout -k 10 900 python -u bench.py > gpurun_out/r04h2_bench.log 2>&1 || exit $?
+grep '^{' gpurun_out/r04h2_bench.log > gpurun_out/r04h2_bench.json
 python3 - <<'PY'
 import json
-r = json.loads(open("gpurun_out/r04i_bench.json").read().strip().splitlines()[-1])
+r = json.loads(open("gpurun_out/r04h2_bench.json").read().strip().splitlines()[-1])
 print("value", r["value"], r["unit"], "ms/step", r["ms_per_step"])
 print("roofline", {k: r["roofline"].get(k) for k in ("achieved", "frac", "traffic")})
 s2 = r.get("stage2", {})
