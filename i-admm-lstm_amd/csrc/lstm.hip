@@ -104,7 +104,6 @@ extern "C" int iadmm_lstm_cell_fwd(int64_t M, int64_t h, const float* H, const f
   // tile order: groups of 4 row panels, hidden tile slowest (cell_tile_of_block_grouped): bitwise
   // the same result as panel-major order, 29 % fewer L2 misses (tools/cellmap.py, profiles/r02_cellmap_*)
   CellArgsT a{M, (int)h, (int)njt, (int)cdiv(h, kBK), H, C, xv, g, Upk, Wx, Hn, Cn, part, 4};
-  if (const char* e = getenv("IADMM_CELL_PGROUP")) a.pgroup = atoi(e);  // mapping study (tools/cellmap.py)
   const bool vec = (h % 4 == 0) && aligned16(H) && aligned16(C) && aligned16(Hn) && aligned16(Cn);
   const dim3 grid((unsigned)(nrt * njt));
   if (vec) {

@@ -39,7 +39,7 @@
 // pivot (0 = non-singular), LAPACK convention.
 #include <algorithm>
 #include <cstdlib>
-#include <mutex>
+#include <new>
 #include <type_traits>
 
 #include "common.h"
@@ -911,16 +911,16 @@ __global__ __launch_bounds__(kTrailThreads, 1) void lu_trail_kernel(int N, int K
 // 16 flop/B, under the fp32 MFMA ridge; per 128-column block [P, P + 128) the two 64-column halves
 // are factored one after the other (the second half updated by the first: the rank-64 "mid" update
 // of lu_trail_kernel restricted to [P + 64, P + 128)), and the rest of the matrix gets ONE rank-128
-// update: half the A22 traffic, 32 flop/B.  U12 = L11^-1 A12 for the 128 block rows is an MFMA
-// product with the explicitly inverted unit-lower L11 (lu_linv_kernel), fused into the trailing
-// update's prologue (every strip's workgroup owns its 128 columns of A12 and A22, so no other
+// update: half the A22 traffic, 32 flop/B.  U12 = L11^-1 A12 for the 128 block rows is a two-level
+// MFMA substitution with the inverted 32 x 32 diagonal blocks of L11 (lu_linv_kernel, r05), fused into
+// the trailing update's prologue (every strip's workgroup owns its 128 columns of A12 and A22, so no other
 // workgroup reads what it overwrites).
 constexpr int kOB = 2 * kBlk;     // outer block width = rank of the fused trailing update
 constexpr int kT2C = 128;         // trailing update: columns per workgroup strip
 constexpr int kT2S = 32;          //   rows per pipeline step
 constexpr int kT2K = kOB + 4;     //   LDS stride (k) of the U12^T and L21 tiles
 constexpr int kT2CS = kT2C + 8;   //   LDS stride of the product tile
-constexpr int kT2PK = kOB / 2 + 4;  //   LDS stride of the prologue's 64-k half tiles
+constexpr int kT2LK = kOB + 4;    //   LDS stride of the prologue's staged two-level L11^-1
 constexpr int kT2Threads = 256;   // 4 waves; two workgroups per CU
 // the block's composed row permutation for the gathered loads: the block rows' sources, the displaced
 // rows below the block with their sources (as given, then sorted by row), a bitmap of the displaced
@@ -928,7 +928,7 @@ constexpr int kT2Threads = 256;   // 4 waves; two workgroups per CU
 constexpr int kT2BitWords = (kLuMaxN + kT2S - 1) / kT2S + 2;
 // L21 and the product tile double-buffered; the prologue's half tiles and U12^T over them
 constexpr int kT2MainFloats = 2 * kT2S * kT2K + 2 * kT2S * kT2CS;
-constexpr int kT2ProFloats = 2 * kOB * kT2PK;
+constexpr int kT2ProFloats = kOB * kT2LK;
 constexpr int kT2AreaFloats = kT2MainFloats > kT2ProFloats ? kT2MainFloats : kT2ProFloats;
 constexpr size_t kT2Lds = (size_t)kT2AreaFloats * sizeof(float) + (size_t)(4 * kPermMax + kT2BitWords) * sizeof(int) +
                           (size_t)((kT2BitWords + 3) & ~3);
@@ -937,13 +937,18 @@ static_assert(kT2C == 128 && kOB == 128, "the wave layout assumes a 128 x 128 bl
 static_assert(2 * kT2Lds <= 160 * 1024, "two workgroups per CU (gfx950 LDS)");
 constexpr int kLinvFloats = kOB * kOB;
 
-// Linv[b] = (unit lower part of A[P:P+128, P:P+128])^-1, row-major 128 x 128.  Thread j computes
-// column j by forward substitution x_i = -sum_{k<i} L_ik x_k (x_k = 0 for k < j, x_j = 1) with the
-// column in registers (both loops unrolled) and L broadcast from LDS 4 entries per read; four
-// partial sums per row shorten the dependent chains.  (r03 first form: L and X both in LDS, one
-// workgroup per CU, LDS-latency bound: 1.6 ms per block at B = 1024, 15x this one.)
+// Two-level L11^-1 of the block's 128 x 128 unit-lower factor (r05), row-major 128 x 128 into Linv[b]:
+// the four 32 x 32 diagonal blocks inverted (Linv_jj), the blocks below them as -L_ij, zeros above.
+// lu_trail128_kernel's prologue then forms U12 block row by block row, U_j = Linv_jj (A_j - sum_{i<j}
+// L_ji U_i): substitution between the 32-row blocks, explicit inverses only within them.  (r04: the
+// explicit inverse of the whole 128 x 128 factor; its residual grows with kappa(L11) where
+// substitution's does not -- the factorization's backward error was 1.6-1.8x MKL sgetrf's on the
+// KKT matrices, 0.95-1.0x with the two-level form: tools/lu_accuracy_sim.py,
+// profiles/r05_lu_accuracy_sim_N2000.txt.)  Thread j computes column j % 32 of its diagonal block by
+// forward substitution (one fmaf chain per entry, L broadcast from LDS) and writes column j.
 // perm != nullptr (r04, look-ahead): a third wave builds the block's composed permutation (what
 // lu_block_perm_kernel does) beside the substitution, one launch less on the critical path.
+constexpr int kLd = 32;  // diagonal block of the two-level inverse
 __global__ __launch_bounds__(kOB + 64) void lu_linv_kernel(int N, int P, const float* A, float* Linv, const int* piv,
                                                          int* perm, int cend) {
   __shared__ __attribute__((aligned(16))) float L[kOB][kOB + 4];
@@ -981,24 +986,23 @@ __global__ __launch_bounds__(kOB + 64) void lu_linv_kernel(int N, int P, const f
     }
   }
   __syncthreads();
-  float x[kOB];
+  const int d0 = j & ~(kLd - 1), jj = j - d0;  // this column's diagonal block [d0, d0 + 32)
+  float x[kLd];
 #pragma unroll
-  for (int i = 0; i < kOB; ++i) {
-    float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+  for (int i = 0; i < kLd; ++i) {
+    float s = i == jj ? 1.f : 0.f;
 #pragma unroll
-    for (int k4 = 0; k4 < (i & ~3); k4 += 4) {
-      const float4 l = *reinterpret_cast<const float4*>(&L[i][k4]);
-      s0 = fmaf(l.x, x[k4], s0); s1 = fmaf(l.y, x[k4 + 1], s1);
-      s2 = fmaf(l.z, x[k4 + 2], s2); s3 = fmaf(l.w, x[k4 + 3], s3);
-    }
-#pragma unroll
-    for (int k = i & ~3; k < i; ++k) s0 = fmaf(L[i][k], x[k], s0);
-    const float v = -((s0 + s1) + (s2 + s3));
-    x[i] = i < j ? 0.f : (i == j ? 1.f : v);
+    for (int k = 0; k < i; ++k) s = fmaf(-L[d0 + i][d0 + k], x[k], s);
+    x[i] = i < jj ? 0.f : s;
   }
   float* out = Linv + b * (size_t)kLinvFloats;
 #pragma unroll
-  for (int i = 0; i < kOB; ++i) out[i * kOB + j] = x[i];
+  for (int bi = 0; bi < kOB / kLd; ++bi)
+#pragma unroll
+    for (int t = 0; t < kLd; ++t) {
+      const int i = bi * kLd + t;
+      out[i * kOB + j] = kLd * bi == d0 ? x[t] : (kLd * bi > d0 ? -L[i][j] : 0.f);
+    }
 }
 
 // Fused row interchanges, U12 = L11^-1 A12 and A22 -= L21 U12 (rank 128) for the columns right of
@@ -1012,11 +1016,10 @@ __global__ __launch_bounds__(kOB + 64) void lu_linv_kernel(int N, int P, const f
 // overwritten (with U12) after the last step's loads.  A displaced row finds its source in O(1):
 // sources sorted by row (dsrc), the rank of a step's first displaced row (dpre) plus the popcount
 // of the step's bitmap below the row.  (perm == nullptr: no interchanges, tools/lubench128.hip.)
-//   prologue: U12 = L11^-1 A12 on MFMA in two passes of 64 k (the L11^-1 columns and gathered A12
-//             rows of MFMA k-steps [8p, 8p + 8) of both lane halves; wave w: U12 rows [32w, 32w+32),
-//             four 32 x 32 tiles accumulating across the passes), transposed into LDS, then each
-//             wave's MFMA operand -- column 32w + il, k in [64h, 64h + 64): 64 registers -- kept in
-//             registers for the whole loop;
+//   prologue: U12 = L11^-1 A12 on MFMA by 32-row blocks (two-level, r05: U_j = Linv_jj (A_j -
+//             sum_{i<j} L_ji U_i); wave w: strip columns [32w, 32w + 32), no exchange between waves),
+//             transposed into LDS, then each wave's MFMA operand for the main loop -- column 32w + il,
+//             k in [64h, 64h + 64): 64 registers -- kept in registers for the whole loop;
 //   main loop: 32-row steps; wave w owns columns [32w, 32w + 32) of a step (v_mfma_f32_32x32x2f32,
 //             64 per step, the first on an inline-zero C, L21 fragments read two k-groups ahead,
 //             U12 from registers).  L21 and the product tile are double-buffered in LDS, so a step
@@ -1024,7 +1027,7 @@ __global__ __launch_bounds__(kOB + 64) void lu_linv_kernel(int N, int P, const f
 //             MFMAs; product -> Cb[t & 1]; L21 (t + 1) -> Ls[(t + 1) & 1]; barrier; out = A22 -
 //             product for step t (row-contiguous global stores, the A22 values already in the
 //             registers of the storing thread).
-// Same MFMA chains, products and subtractions as the r03 kernel: bitwise the same factors.
+// Main loop: the same MFMA chains, products and subtractions as the r03 kernel.
 // Strips of one instance are consecutive logical ids on one XCD (its L2 serves the L21 re-reads).
 // DIAG (tools/lubench128.hip only): 1 = no MFMAs in the main loop, 2 = no global A22 / L21 traffic in it.
 template <bool VEC, int DIAG = 0>
@@ -1033,9 +1036,7 @@ __global__ __launch_bounds__(kT2Threads, 2) void lu_trail128_kernel(int N, int P
   extern __shared__ __attribute__((aligned(16))) float sm[];
   float* Ls0 = sm;                      // 2 x [kT2S rows][kT2K]: L21 of a step
   float* Cb0 = sm + 2 * kT2S * kT2K;    // 2 x [kT2S rows][kT2CS]: product of a step
-  float* Lh = sm;                       // prologue pass: its L11^-1 columns [128 rows][kT2PK]
-  float* Uh = sm + kOB * kT2PK;         //                its A12 rows, transposed [128 cols][kT2PK]
-  float* Ut = sm;                       // then U12^T [128 cols][kT2K]
+  float* Ut = sm;                       // after the prologue: U12^T [128 cols][kT2K]
   int* bsrc = reinterpret_cast<int*>(sm + kT2AreaFloats);  // [128] source row of block row P + i
   int* tdst = bsrc + kPermMax;          // [128] displaced rows and
   int* tsrc = tdst + kPermMax;          // [128] their sources, as given;
@@ -1058,7 +1059,6 @@ __global__ __launch_bounds__(kT2Threads, 2) void lu_trail128_kernel(int N, int P
   constexpr int W = VEC ? 4 : 1;
   constexpr int kCQ = kT2S * kT2C / W / NT;   // A22 accesses per thread per step
   constexpr int kLQ = kT2S * kOB / W / NT;    // L21 accesses per thread per step
-  constexpr int kAQ = (kOB / 2) * kT2C / W / NT;  // A12 accesses per thread per prologue pass
   constexpr int CPR = kT2C / W, LPR = kOB / W;
   // main-loop loads: unconditional, from a clamped (valid) address.  Rows >= N / columns >= N only
   // feed products that are never stored, so they need no zero fill -- and a load with no select
@@ -1092,67 +1092,67 @@ __global__ __launch_bounds__(kT2Threads, 2) void lu_trail128_kernel(int N, int P
     dpre[dd >> 5] = (unsigned char)drank;
   // (published by the prologue's barriers)
 
-  // ---- prologue: U12 = L11^-1 A12 on this strip; wave w: U12 rows [32w, 32w + 32)
+  // ---- prologue (r05, two-level): U12 = L11^-1 A12 on this strip by 32-row blocks,
+  // U_j = Linv_jj (A_j - sum_{i<j} L_ji U_i) (lu_linv_kernel's layout: Linv_jj on the diagonal, -L_ji
+  // below).  Wave w owns the strip's columns [32w, 32w + 32) for all 128 rows, so it needs no other
+  // wave's result: its U_i are accumulator tiles (lane half h: rows 8q + 4h + r of the block, column
+  // il), and the MFMA k index runs over exactly those rows -- U_i is the B operand straight from
+  // registers, the matching L entries (four consecutive k) one 16-B LDS read.  A_j is the first
+  // MFMA's C operand (the gathered block rows, loaded in accumulator layout).
   const float* Lb = Linv + b * (size_t)kLinvFloats;
-  floatx16 u[4];
+  float* Lt = sm;  // [128 rows][kT2LK]: Lb staged
+  {
+    float4 lv[kOB * kOB / 4 / NT];
 #pragma unroll
-  for (int j = 0; j < 4; ++j)
-#pragma unroll
-    for (int v = 0; v < 16; ++v) u[j][v] = 0.f;
-#pragma unroll
-  for (int pass = 0; pass < 2; ++pass) {
-    // pass-local k index kk in [0, 64): kk < 32 -> k = 32 pass + kk, else k = 64 + 32 pass + kk - 32
-    if (pass) __syncthreads();  // the first pass's tiles consumed
-    VT av[kAQ];
-    float4 lv[8];
-#pragma unroll
-    for (int q = 0; q < kAQ; ++q) {  // the pass's A12 rows (64 k x 128 columns), gathered
-      const int e = tid + NT * q, kk = e / CPR, col = cb + (e % CPR) * W;
-      const int k = kk < 32 ? 32 * pass + kk : 64 + 32 * pass + kk - 32;
-      const VT x = ldu(bsrc[k], min(col, N - W));
-      if constexpr (VEC) av[q] = col < N ? x : make_float4(0.f, 0.f, 0.f, 0.f);
-      else av[q] = col < N ? x : 0.f;
-    }
-#pragma unroll
-    for (int q = 0; q < 8; ++q) {  // the pass's L11^-1 columns (128 rows x 64 k), 16-B pieces
-      const int e = tid + NT * q, i = e / 16, kk = (e % 16) * 4;
-      const int k = kk < 32 ? 32 * pass + kk : 64 + 32 * pass + kk - 32;
-      lv[q] = *reinterpret_cast<const float4*>(Lb + (size_t)i * kOB + k);
-    }
-#pragma unroll
-    for (int q = 0; q < kAQ; ++q) {
-      const int e = tid + NT * q, kk = e / CPR, cl = (e % CPR) * W;
-      if constexpr (VEC) {
-        Uh[(cl + 0) * kT2PK + kk] = av[q].x; Uh[(cl + 1) * kT2PK + kk] = av[q].y;
-        Uh[(cl + 2) * kT2PK + kk] = av[q].z; Uh[(cl + 3) * kT2PK + kk] = av[q].w;
-      } else {
-        Uh[cl * kT2PK + kk] = av[q];
-      }
-    }
-#pragma unroll
-    for (int q = 0; q < 8; ++q) {
+    for (int q = 0; q < kOB * kOB / 4 / NT; ++q) {
       const int e = tid + NT * q;
-      *reinterpret_cast<float4*>(Lh + (e / 16) * kT2PK + (e % 16) * 4) = lv[q];
+      lv[q] = *reinterpret_cast<const float4*>(Lb + (size_t)(e / (kOB / 4)) * kOB + (e % (kOB / 4)) * 4);
     }
-    __syncthreads();
-#pragma unroll 2
-    for (int sg = 0; sg < 8; ++sg) {
-      const float4 fa = *reinterpret_cast<const float4*>(Lh + (wave * 32 + il) * kT2PK + 32 * h + 4 * sg);
-      float4 fb[4];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) fb[j] = *reinterpret_cast<const float4*>(Uh + (j * 32 + il) * kT2PK + 32 * h + 4 * sg);
-#pragma unroll
-      for (int s4 = 0; s4 < 4; ++s4)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) u[j] = __builtin_amdgcn_mfma_f32_32x32x2f32(get4(fa, s4), get4(fb[j], s4), u[j], 0, 0, 0);
+    for (int q = 0; q < kOB * kOB / 4 / NT; ++q) {
+      const int e = tid + NT * q;
+      *reinterpret_cast<float4*>(Lt + (e / (kOB / 4)) * kT2LK + (e % (kOB / 4)) * 4) = lv[q];
     }
   }
+  floatx16 u[4];
+  {
+    // (columns >= N: clamped loads, never stored -- a column of U12 feeds only its own column)
+    const int colc = min(cb + 32 * wave + il, N - 1);
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int v = 0; v < 16; ++v)
+        u[j][v] = Ab[(size_t)bsrc[32 * j + 8 * (v >> 2) + 4 * h + (v & 3)] * N + colc];
+  }
+  __syncthreads();  // Lt staged
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    floatx16 acc = u[j];
+#pragma unroll
+    for (int i = 0; i < j; ++i)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float4 l4 = *reinterpret_cast<const float4*>(Lt + (32 * j + il) * kT2LK + 32 * i + 8 * q + 4 * h);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(get4(l4, r), u[i][4 * q + r], acc, 0, 0, 0);
+      }
+    const floatx16 zero = {};
+    floatx16 o = zero;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const float4 l4 = *reinterpret_cast<const float4*>(Lt + (32 * j + il) * kT2LK + 32 * j + 8 * q + 4 * h);
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        o = __builtin_amdgcn_mfma_f32_32x32x2f32(get4(l4, r), acc[4 * q + r], (q == 0 && r == 0) ? zero : o, 0, 0, 0);
+    }
+    u[j] = o;
+  }
   __syncthreads();  // the pass tiles consumed: U12^T over them
-  // accumulator v of tile j <-> U12 row 32w + 8(v/4) + 4h + v%4, strip column 32j + il
+  // accumulator v of tile j <-> U12 row 32j + 8(v/4) + 4h + v%4, strip column 32w + il
 #pragma unroll
   for (int j = 0; j < 4; ++j)
 #pragma unroll
-    for (int v = 0; v < 16; ++v) Ut[(j * 32 + il) * kT2K + wave * 32 + 8 * (v >> 2) + 4 * h + (v & 3)] = u[j][v];
+    for (int v = 0; v < 16; ++v) Ut[(wave * 32 + il) * kT2K + 32 * j + 8 * (v >> 2) + 4 * h + (v & 3)] = u[j][v];
   __syncthreads();
   const int wc = wave * 32;
   float4 ub[kOB / 8];  // U12[64h + 4sg + 0..3][wc + il]: this wave's MFMA operand for every step
@@ -1630,53 +1630,21 @@ static int lu_rank64(int64_t B, int64_t N, int K0, int cend, int cmax, float* A,
   return 0;
 }
 
-// The look-ahead's streams and events, per device, made on first use (non-blocking: no implicit
-// synchronisation with the null stream); the mutex keeps one factorization at a time on them.  s1
-// (the device's highest priority) carries the critical path -- the block factorizations and the
-// strips the next block needs -- and s2 (lowest) the rest of each trailing update, so that CUs
-// freed by s2's workgroups go to s1's first.  The caller's stream forks into s1 and joins it at
-// the end.
-struct LuSide {
-  std::mutex mu;
+// The look-ahead's streams and events (r05: a caller-owned context, iadmm_lu_ctx_create; r04 kept
+// them in library statics behind a mutex, against the header's contract).  s1 (the device's highest
+// priority) carries the critical path -- the block factorizations and the strips the next block
+// needs -- and s2 (lowest) the rest of each trailing update, so that CUs freed by s2's workgroups go
+// to s1's first.  The caller's stream forks into s1 and joins it at the end; every path out of
+// lu_factor_blocks after the fork runs that join (the caller may free A, piv and ws on its stream
+// as soon as the call returns).
+struct iadmm_lu_ctx {
+  int device = -1;
   hipStream_t s1 = nullptr, s2 = nullptr;
   hipEvent_t fork = nullptr, join = nullptr, ev0 = nullptr, ev1 = nullptr;
 };
-static LuSide* lu_side() {
-  static std::mutex mk;
-  static LuSide side[64];
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
-  std::lock_guard<std::mutex> g(mk);
-  LuSide& d = side[dev];
-  if (!d.s2) {
-    int least = 0, greatest = 0;
-    if (hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess) least = greatest = 0;
-    hipStream_t a = nullptr, c = nullptr;
-    hipEvent_t e[4] = {};
-    if (hipStreamCreateWithPriority(&a, hipStreamNonBlocking, greatest) != hipSuccess) return nullptr;
-    if (hipStreamCreateWithPriority(&c, hipStreamNonBlocking, least) != hipSuccess) {
-      (void)hipStreamDestroy(a);
-      return nullptr;
-    }
-    for (int i = 0; i < 4; ++i)
-      if (hipEventCreateWithFlags(&e[i], hipEventDisableTiming) != hipSuccess) {
-        for (int k = 0; k < i; ++k) (void)hipEventDestroy(e[k]);
-        (void)hipStreamDestroy(a);
-        (void)hipStreamDestroy(c);
-        return nullptr;
-      }
-    d.fork = e[0];
-    d.join = e[1];
-    d.ev0 = e[2];
-    d.ev1 = e[3];
-    d.s1 = a;
-    d.s2 = c;
-  }
-  return &d;
-}
 
 static int lu_factor_blocks(int64_t B, int64_t N, float* A, int* piv, int* info, int* perm, int* sig, float* linv,
-                            hipStream_t s0, bool gather) {
+                            hipStream_t s0, bool gather, iadmm_lu_ctx* ctx) {
   hipStream_t s = s0;
   const bool vec = (N % 4 == 0) && aligned16(A);
   IADMM_ALLOW_LDS(lu_trail_kernel<true>, kTrailLds);
@@ -1694,16 +1662,30 @@ static int lu_factor_blocks(int64_t B, int64_t N, float* A, int* piv, int* info,
   // in-block updates and L11^-1, which touch only block t + 1's columns once the left interchanges
   // are deferred, run beside the rest of block t's update; block t + 1's trailing update waits for
   // it.  L11^-1 alternates between two buffers (the side launch of block t still reads its own).
-  LuSide* side = defer ? lu_side() : nullptr;
-  std::unique_lock<std::mutex> side_lock;
+  // (without a context, or above N = 2048, everything runs in order on the caller's stream)
+  iadmm_lu_ctx* side = defer ? ctx : nullptr;
   if (side) {
-    side_lock = std::unique_lock<std::mutex>(side->mu);
+    // Under stream capture every launch stays on the caller's stream (same factors, bit for bit):
+    // capturing the fork / join across the context's two streams crashed the HIP 7.2 runtime in
+    // hipStreamEndCapture (gpurun r05a, torch.cuda.graph around ops.lu_factor).
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    IADMM_HIP_RC(hipStreamIsCapturing(s0, &cs));
+    if (cs != hipStreamCaptureStatusNone) side = nullptr;
+  }
+  if (side) {  // (nothing is enqueued on s1 before both calls succeed: a failure returns unforked)
     IADMM_HIP_RC(hipEventRecord(side->ev0, s0));
     IADMM_HIP_RC(hipStreamWaitEvent(side->s1, side->ev0, 0));
     s = side->s1;
   }
   bool pending = false;  // a side launch not yet joined
   int rc = 0;
+  // after the fork no error may return early: record it, leave the loop, and still join below
+#define LU_TRY(call)                              \
+  {                                               \
+    const hipError_t e_ = (call);                 \
+    if (e_ != hipSuccess) { rc = (int)e_; break; } \
+  }
+#define LU_TRY_LAUNCH() LU_TRY(hipGetLastError())
   for (int P = 0; P < N && !rc; P += kOB) {
     const int n_ = (int)N;
     const int c1 = std::min(n_, P + kBlk), c2 = std::min(n_, P + kOB);
@@ -1725,7 +1707,7 @@ static int lu_factor_blocks(int64_t B, int64_t N, float* A, int* piv, int* info,
     const bool perm_in_linv = defer && c2 < n_;
     if (!perm_in_linv) {
       hipLaunchKernelGGL(lu_block_perm_kernel, dim3((unsigned)B), dim3(64), 0, s, (int)N, P, c2, piv, pm);
-      IADMM_CHECK_LAUNCH();
+      LU_TRY_LAUNCH();
     }
     rc = lu_swap(B, N, P, c2, 0, defer ? 0 : P, gather ? 0 : c2, gather ? 0 : n_, 0, A, piv, pm, s, false);
     if (rc || c2 >= n_) break;
@@ -1733,7 +1715,7 @@ static int lu_factor_blocks(int64_t B, int64_t N, float* A, int* piv, int* info,
     float* lv = linv + (side ? ((P / kOB) & 1) * B * (int64_t)kLinvFloats : 0);
     hipLaunchKernelGGL(lu_linv_kernel, dim3((unsigned)B), dim3(kOB + 64), 0, s, (int)N, P, A, lv, piv,
                        perm_in_linv ? pm : nullptr, c2);
-    IADMM_CHECK_LAUNCH();
+    LU_TRY_LAUNCH();
     const int ntc = ((int)N - c2 + kT2C - 1) / kT2C;
     const int* gp = gather ? pm : nullptr;
     auto trail = [&](hipStream_t st, int tc0, int cnt) {
@@ -1743,38 +1725,46 @@ static int lu_factor_blocks(int64_t B, int64_t N, float* A, int* piv, int* info,
     };
     if (!side) {
       trail(s, 0, ntc);
-      IADMM_CHECK_LAUNCH();
+      LU_TRY_LAUNCH();
       continue;
     }
-    if (pending) IADMM_HIP_RC(hipStreamWaitEvent(s, side->join, 0));  // block t - 1's other strips
-    pending = false;
+    if (pending) {  // block t - 1's other strips
+      LU_TRY(hipStreamWaitEvent(s, side->join, 0));
+      pending = false;
+    }
     if (ntc > 1) {
-      IADMM_HIP_RC(hipEventRecord(side->fork, s));
-      IADMM_HIP_RC(hipStreamWaitEvent(side->s2, side->fork, 0));
+      LU_TRY(hipEventRecord(side->fork, s));
+      LU_TRY(hipStreamWaitEvent(side->s2, side->fork, 0));
       trail(side->s2, 1, ntc - 1);
-      IADMM_CHECK_LAUNCH();
-      IADMM_HIP_RC(hipEventRecord(side->join, side->s2));
+      const hipError_t e = hipGetLastError();
+      // (join even after a failed launch: whatever reached s2 is ordered before the caller's stream)
+      LU_TRY(hipEventRecord(side->join, side->s2));
       pending = true;
+      LU_TRY(e);
     }
     trail(s, 0, 1);
-    IADMM_CHECK_LAUNCH();
+    LU_TRY_LAUNCH();
   }
-  if (pending) {
-    const hipError_t e = hipStreamWaitEvent(s, side->join, 0);
+#undef LU_TRY
+#undef LU_TRY_LAUNCH
+  auto keep = [&rc](hipError_t e) {  // the first error wins
     if (e != hipSuccess && !rc) rc = (int)e;
-  }
+  };
+  if (pending && !rc && hipStreamWaitEvent(s, side->join, 0) == hipSuccess) pending = false;
   if (!rc && defer && nb > 1) {
     hipLaunchKernelGGL(lu_left_compose_kernel, dim3((unsigned)B), dim3(64), 0, s, (int)N, nb, slot, perm, sig);
-    IADMM_CHECK_LAUNCH();
-    const dim3 grid((unsigned)(B * 8 * (nb - 1)));
-    if (vec) hipLaunchKernelGGL(lu_left_apply_kernel<true>, grid, dim3(512), 0, s, (int)N, nb - 1, sig, A);
-    else hipLaunchKernelGGL(lu_left_apply_kernel<false>, grid, dim3(512), 0, s, (int)N, nb - 1, sig, A);
-    IADMM_CHECK_LAUNCH();
+    keep(hipGetLastError());
+    if (!rc) {
+      const dim3 grid((unsigned)(B * 8 * (nb - 1)));
+      if (vec) hipLaunchKernelGGL(lu_left_apply_kernel<true>, grid, dim3(512), 0, s, (int)N, nb - 1, sig, A);
+      else hipLaunchKernelGGL(lu_left_apply_kernel<false>, grid, dim3(512), 0, s, (int)N, nb - 1, sig, A);
+      keep(hipGetLastError());
+    }
   }
-  if (side) {  // the caller's stream joins s1 (which has joined s2)
+  if (side) {  // the caller's stream joins s1 -- and s2 directly if s1 has not -- on every path after the fork
     const hipError_t e1 = hipEventRecord(side->ev1, s);
-    const hipError_t e2 = e1 == hipSuccess ? hipStreamWaitEvent(s0, side->ev1, 0) : e1;
-    if (e2 != hipSuccess && !rc) rc = (int)e2;
+    keep(e1 == hipSuccess ? hipStreamWaitEvent(s0, side->ev1, 0) : e1);
+    if (pending) keep(hipStreamWaitEvent(s0, side->join, 0));
   }
   return rc;
 }
@@ -1872,14 +1862,6 @@ __global__ __launch_bounds__(256) void lu_solve_gemv_kernel(int N, const float* 
   }
 }
 
-// (test hook: IADMM_LU_FORCE_HBM=1 sends every size through the HBM forms -- the interchange pass
-// instead of the gathered trailing-update loads, and the multi-launch solve -- so tests can compare
-// them with the LDS-resident forms at sizes that have both)
-static bool lu_force_hbm() {
-  const char* e = getenv("IADMM_LU_FORCE_HBM");
-  return e && e[0] == '1';
-}
-
 static int lu_solve_hbm(int64_t B, int64_t N, const float* LU, const int* piv, float* x, hipStream_t s) {
   const bool vec = N % 4 == 0 && aligned16(LU);
   hipLaunchKernelGGL(lu_solve_perm_kernel, dim3((unsigned)B), dim3(64), 0, s, (int)N, piv, x);
@@ -1931,30 +1913,76 @@ extern "C" int64_t iadmm_lu_factor_ws_bytes(int64_t B, int64_t N) {
   return lu_ws_bytes(B, N);
 }
 
-extern "C" int iadmm_lu_factor(int64_t B, int64_t N, float* A, int* piv, int* info, void* ws, int64_t ws_bytes,
-                               void* stream) {
+extern "C" int iadmm_lu_ctx_create(iadmm_lu_ctx** out) {
+  if (!out) return IADMM_E_ARG;
+  *out = nullptr;
+  iadmm_lu_ctx* c = new (std::nothrow) iadmm_lu_ctx();
+  if (!c) return (int)hipErrorOutOfMemory;
+  hipError_t e = hipGetDevice(&c->device);
+  int least = 0, greatest = 0;
+  if (e == hipSuccess && hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess) least = greatest = 0;
+  if (e == hipSuccess) e = hipStreamCreateWithPriority(&c->s1, hipStreamNonBlocking, greatest);
+  if (e == hipSuccess) e = hipStreamCreateWithPriority(&c->s2, hipStreamNonBlocking, least);
+  hipEvent_t* evs[4] = {&c->fork, &c->join, &c->ev0, &c->ev1};
+  for (int i = 0; i < 4 && e == hipSuccess; ++i) e = hipEventCreateWithFlags(evs[i], hipEventDisableTiming);
+  if (e != hipSuccess) {
+    (void)iadmm_lu_ctx_destroy(c);
+    return (int)e;
+  }
+  *out = c;
+  return 0;
+}
+
+extern "C" int iadmm_lu_ctx_destroy(iadmm_lu_ctx* c) {
+  if (!c) return 0;
+  hipError_t first = hipSuccess;
+  auto keep = [&first](hipError_t e) { if (first == hipSuccess) first = e; };
+  for (hipEvent_t ev : {c->fork, c->join, c->ev0, c->ev1})
+    if (ev) keep(hipEventDestroy(ev));
+  for (hipStream_t st : {c->s1, c->s2})
+    if (st) keep(hipStreamDestroy(st));  // (returns once the stream's work is done)
+  delete c;
+  return (int)first;
+}
+
+extern "C" int iadmm_lu_factor_ex(int64_t B, int64_t N, float* A, int* piv, int* info, void* ws, int64_t ws_bytes,
+                                  iadmm_lu_ctx* ctx, int flags, void* stream) {
   if (B <= 0 || N <= 0 || !A || !piv || !info || !ws) return IADMM_E_ARG;
   if (ws_bytes < lu_ws_bytes(B, N)) return IADMM_E_ARG;
+  if (flags & ~IADMM_LU_FORCE_HBM) return IADMM_E_ARG;
   if (!aligned16(ws)) return IADMM_E_ALIGN;
   if (N > kLuMaxHbmN || B > 0x7fffffff) return IADMM_E_SIZE;
   const int64_t ntc_max = (N + kTC - 1) / kTC, nrc_max = (N + kTRW - 1) / kTRW;
   if (B * ntc_max * nrc_max > 0x7fffffff) return IADMM_E_SIZE;
+  if (ctx) {  // a context belongs to the device it was made on
+    int dev = -1;
+    const hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return (int)e;
+    if (dev != ctx->device) return IADMM_E_ARG;
+  }
   hipStream_t s = (hipStream_t)stream;
   const hipError_t e = hipMemsetAsync(info, 0, B * sizeof(int), s);
   if (e != hipSuccess) return (int)e;
   int* perm = static_cast<int*>(ws);
   int* sig = reinterpret_cast<int*>(static_cast<char*>(ws) + lu_perm_bytes(B, N));
   float* linv = reinterpret_cast<float*>(static_cast<char*>(ws) + lu_perm_bytes(B, N) + lu_sig_bytes(B, N));
-  return lu_factor_blocks(B, N, A, piv, info, perm, sig, linv, s, N <= kLuMaxN && !lu_force_hbm());
+  const bool gather = N <= kLuMaxN && !(flags & IADMM_LU_FORCE_HBM);
+  return lu_factor_blocks(B, N, A, piv, info, perm, sig, linv, s, gather, ctx);
 }
 
-extern "C" int iadmm_lu_solve(int64_t B, int64_t N, const float* LU, const int* piv, float* x,
-                              void* stream) {
+extern "C" int iadmm_lu_factor(int64_t B, int64_t N, float* A, int* piv, int* info, void* ws, int64_t ws_bytes,
+                               void* stream) {
+  return iadmm_lu_factor_ex(B, N, A, piv, info, ws, ws_bytes, nullptr, 0, stream);
+}
+
+extern "C" int iadmm_lu_solve_ex(int64_t B, int64_t N, const float* LU, const int* piv, float* x, int flags,
+                                 void* stream) {
   if (B <= 0 || N <= 0 || !LU || !piv || !x) return IADMM_E_ARG;
+  if (flags & ~IADMM_LU_FORCE_HBM) return IADMM_E_ARG;
   const size_t lds = ((size_t)N + kSolveBlk + kSolveBlk * kDS) * sizeof(float);
   if (N > kLuMaxHbmN || B > 0x7fffffff || B * ((N + 63) / 64) > 0x7fffffff) return IADMM_E_SIZE;
   // gfx950: 160 KiB of LDS per workgroup; x beyond it lives in HBM
-  if (lds > 160 * 1024 || lu_force_hbm()) return lu_solve_hbm(B, N, LU, piv, x, (hipStream_t)stream);
+  if (lds > 160 * 1024 || (flags & IADMM_LU_FORCE_HBM)) return lu_solve_hbm(B, N, LU, piv, x, (hipStream_t)stream);
   IADMM_ALLOW_LDS(lu_solve_kernel<true>, lds);
   IADMM_ALLOW_LDS(lu_solve_kernel<false>, lds);
   int dev = 0, cus = 256;
@@ -1975,6 +2003,10 @@ extern "C" int iadmm_lu_solve(int64_t B, int64_t N, const float* LU, const int* 
                        (int)N, LU, piv, x);
   IADMM_CHECK_LAUNCH();
   return 0;
+}
+
+extern "C" int iadmm_lu_solve(int64_t B, int64_t N, const float* LU, const int* piv, float* x, void* stream) {
+  return iadmm_lu_solve_ex(B, N, LU, piv, x, 0, stream);
 }
 
 extern "C" int iadmm_kkt_rhs(int64_t B, int64_t n, int64_t m, int64_t num_ineq, const float* p,

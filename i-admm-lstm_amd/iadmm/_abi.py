@@ -42,8 +42,12 @@ SIGNATURES = {
     "iadmm_bmv_t": (cint, [i64, i64, i64, vp, vp, vp, vp]),
     "iadmm_bger": (cint, [i64, i64, i64, vp, vp, cint, vp, vp]),
     "iadmm_lu_factor_ws_bytes": (i64, [i64, i64]),
+    "iadmm_lu_ctx_create": (cint, [ctypes.POINTER(vp)]),
+    "iadmm_lu_ctx_destroy": (cint, [vp]),
     "iadmm_lu_factor": (cint, [i64, i64, vp, vp, vp, vp, i64, vp]),
+    "iadmm_lu_factor_ex": (cint, [i64, i64, vp, vp, vp, vp, i64, vp, cint, vp]),
     "iadmm_lu_solve": (cint, [i64, i64, vp, vp, vp, vp]),
+    "iadmm_lu_solve_ex": (cint, [i64, i64, vp, vp, vp, cint, vp]),
     "iadmm_kkt_assemble": (cint, [i64, i64, i64, i64, vp, vp, f32, vp, vp, vp, vp]),
     "iadmm_kkt_rhs": (cint, [i64, i64, i64, i64, vp, vp, vp, vp, f32, vp, vp, vp, vp]),
     "iadmm_kkt_matvec": (cint, [i64, i64, i64, i64, vp, vp, vp, f32, vp, vp, cint, vp, vp]),

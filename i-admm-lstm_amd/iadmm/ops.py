@@ -6,6 +6,9 @@ host synchronisation and no CPU path: a CPU tensor or a missing library raises.
 """
 from __future__ import annotations
 
+import ctypes
+import threading
+
 import torch
 
 from . import _abi
@@ -272,21 +275,61 @@ def lu_factor_ws(B, N, device):
     return torch.empty((nbytes + 3) // 4, dtype=torch.float32, device=device)
 
 
-def lu_factor(K, ws=None):
+LU_FORCE_HBM = 1  # include/iadmm.h IADMM_LU_FORCE_HBM (tests)
+
+
+class LuContext:
+    """An iadmm_lu_ctx: the look-ahead's two priority streams and four events, owned by the caller
+    (include/iadmm.h).  Made on the current device; destroyed with the object."""
+
+    def __init__(self):
+        h = ctypes.c_void_p()
+        _abi.call("iadmm_lu_ctx_create", ctypes.byref(h))
+        self.handle = h.value
+        self.device = torch.cuda.current_device()
+
+    def __del__(self):
+        h, self.handle = getattr(self, "handle", None), None
+        if h and _abi is not None:
+            try:
+                _abi.lib().iadmm_lu_ctx_destroy(h)
+            except Exception:  # interpreter teardown
+                pass
+
+
+_LU_CTX = {}  # (device, caller stream, thread) -> LuContext: one per concurrent caller
+
+
+def lu_context():
+    """The LuContext of the current (device, stream, thread): a context serves one factorization at a
+    time in its streams' order, so concurrent callers -- other threads, other streams, a graph capture
+    beside eager work -- each get their own."""
+    key = (torch.cuda.current_device(), torch.cuda.current_stream().cuda_stream, threading.get_ident())
+    ctx = _LU_CTX.get(key)
+    if ctx is None:
+        ctx = _LU_CTX[key] = LuContext()
+    return ctx
+
+
+def lu_factor(K, ws=None, lookahead=True, flags=0):
     """In-place batched LU with partial pivoting: returns (LU (= K), piv int32 [B,N] 1-based (LAPACK), info int32 [B]).
-    ``ws``: a :func:`lu_factor_ws` buffer (allocated per call when omitted)."""
+    ``ws``: a :func:`lu_factor_ws` buffer (allocated per call when omitted).  ``lookahead``: factor the
+    next block beside each trailing update on this caller's :func:`lu_context` (N <= 2048; the
+    factors are bit for bit the same either way).  ``flags``: 0 or :data:`LU_FORCE_HBM` (tests)."""
     if K.dim() != 3 or K.shape[1] != K.shape[2]:
         raise ValueError(f"K must be [B,N,N], got {tuple(K.shape)}")
     B, N = K.shape[0], K.shape[1]
     piv = torch.empty(B, N, dtype=torch.int32, device=K.device)
     info = torch.empty(B, dtype=torch.int32, device=K.device)
     ws = lu_factor_ws(B, N, K.device) if ws is None else ws
-    _abi.call("iadmm_lu_factor", B, N, _p(K), piv.data_ptr(), info.data_ptr(), _p(ws), ws.numel() * 4, _stream())
+    ctx = lu_context().handle if lookahead else None
+    _abi.call("iadmm_lu_factor_ex", B, N, _p(K), piv.data_ptr(), info.data_ptr(), _p(ws), ws.numel() * 4, ctx,
+              int(flags), _stream())
     return K, piv, info
 
 
-def lu_solve(LU, piv, b):
-    """Solve with (LU, piv) in place on a copy of b [B,N]; returns x."""
+def lu_solve(LU, piv, b, flags=0):
+    """Solve with (LU, piv) in place on a copy of b [B,N]; returns x.  ``flags``: 0 or :data:`LU_FORCE_HBM`."""
     B, N = LU.shape[0], LU.shape[1]
     if LU.dim() != 3 or LU.shape[2] != N:
         raise ValueError(f"LU must be [B,N,N], got {tuple(LU.shape)}")
@@ -298,7 +341,7 @@ def lu_solve(LU, piv, b):
         raise ValueError(f"piv must be [B,N] = [{B},{N}] and b hold B*N values; got piv {tuple(piv.shape)}, "
                          f"b {tuple(b.shape)}")
     x = b.clone().contiguous()
-    _abi.call("iadmm_lu_solve", B, N, _p(LU), piv.data_ptr(), _p(x), _stream())
+    _abi.call("iadmm_lu_solve_ex", B, N, _p(LU), piv.data_ptr(), _p(x), int(flags), _stream())
     return x
 
 

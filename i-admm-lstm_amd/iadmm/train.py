@@ -57,11 +57,20 @@ def ordered_reduce_grads(params, chunk_grads, dist, bucket_bytes=32 << 20):
 
     ``chunk_grads``: this rank's micro-batch gradients in its order, each a list of per-parameter
     tensors (None = no gradient) aligned with ``params``.  Rank r's micro-batches follow rank r-1's
-    in the global order (contiguous shards, parallel.shard)."""
+    in the global order (contiguous shards, parallel.shard).  A parameter that got no gradient in
+    any micro-batch of any rank keeps ``grad = None``, as in one process (so Adam skips it instead
+    of applying weight decay and moment updates to a zero gradient): one small MAX all-reduce of a
+    per-parameter mask."""
     global ALLREDUCE_CALLS
     world, rank = dist.get_world_size(), dist.get_rank()
     params = list(params)
+    if not params:
+        return
     index = {id(p): i for i, p in enumerate(params)}
+    got = torch.tensor([float(any(g[i] is not None for g in chunk_grads)) for i in range(len(params))],
+                       device=params[0].device)
+    dist.all_reduce(got, op=dist.ReduceOp.MAX)
+    got = got.cpu().tolist()
     for bucket in _buckets(params, bucket_bytes):
         ids = [index[id(q)] for q in bucket]
         numel = sum(q.numel() for q in bucket)
@@ -81,9 +90,12 @@ def ordered_reduce_grads(params, chunk_grads, dist, bucket_bytes=32 << 20):
         ALLREDUCE_CALLS += 1
         off = 0
         for q in bucket:
-            if q.grad is None:
-                q.grad = torch.empty_like(q)
-            q.grad.copy_(acc[off:off + q.numel()].view_as(q))
+            if not got[index[id(q)]]:
+                q.grad = None
+            else:
+                if q.grad is None:
+                    q.grad = torch.empty_like(q)
+                q.grad.copy_(acc[off:off + q.numel()].view_as(q))
             off += q.numel()
 
 

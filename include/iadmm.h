@@ -12,8 +12,11 @@
  *     ([B][rows][cols]), unless documented as host.  Integers are int64_t sizes.
  *   - ``stream`` is a hipStream_t passed as void* (0 = legacy default stream).  Calls are
  *     stream-ordered and asynchronous: no allocation, no host synchronisation, no global mutable
- *     state; safe to capture in a hipGraph and to call from several threads on distinct streams.
- *   - Every buffer (outputs and workspaces) is caller-owned.
+ *     state, no environment reads; safe to capture in a hipGraph and to call from several threads
+ *     on distinct streams (tests/test_abi_concurrency_gpu.py).
+ *   - Every buffer (outputs and workspaces) is caller-owned, and so are the only HIP objects the
+ *     library ever creates: the look-ahead streams / events of an iadmm_lu_ctx, made and destroyed
+ *     by the two (not stream-ordered) context calls below.
  *   - Return value: 0 on success; a negative IADMM_E* code for a bad argument or a size beyond
  *     a kernel's limit (nothing is launched); a positive hipError_t if a launch failed.
  *     No C++ exception crosses this boundary.
@@ -114,21 +117,35 @@ int iadmm_kkt_rhs(int64_t B, int64_t n, int64_t m, int64_t num_ineq, const float
  * panels up to N = 2048, 8-column panels on 1024-thread workgroups above, held in registers up to 10240 panel
  * rows and in HBM beyond; rank-128 MFMA trailing update with the block's interchanges as gathered loads up to
  * N = 36736, as a pass of their own above; limit N <= 46340, N * N < 2^31).
- * N <= 2048 (r04): the interchanges left of each block are applied once at the end, and the next block is
- * factored beside the rest of each trailing update (look-ahead) on two library-owned streams of the current
- * device (made once; high / low priority), forked from and joined back into `stream` -- the call stays
- * asynchronous and ordered on `stream`.
+ * N <= 2048 (r04): the interchanges left of each block are applied once at the end.
  * ws: caller-owned, 16-B aligned device workspace of at least iadmm_lu_factor_ws_bytes(B, N) bytes
  * (per-instance block permutations -- one per 128-column block for N <= 2048, with the composed
- * left permutations -- and the 128x128 L11^-1 blocks, two for N <= 2048); nothing is allocated inside. */
+ * left permutations -- and the 128x128 L11^-1 blocks, two for N <= 2048); nothing is allocated inside.
+ * iadmm_lu_factor runs every launch in order on `stream`.  iadmm_lu_factor_ex with a context (N <= 2048)
+ * factors the next block beside the rest of each trailing update (look-ahead) on the context's two
+ * streams (high / low priority), forked from and joined back into `stream` on every path, errors
+ * included: the call stays asynchronous and ordered on `stream`, and the factors are bit for bit
+ * those of iadmm_lu_factor.  Under stream capture (hipGraph) the call ignores the context and runs every
+ * launch on `stream` (the cross-stream fork / join crashed the HIP 7.2 runtime at capture end).  A context belongs to the device current at its creation (IADMM_E_ARG
+ * on another) and serves one factorization at a time in its streams' order: give each concurrent
+ * caller (thread / stream) its own.  flags: 0, or IADMM_LU_FORCE_HBM (tests: the forms for N above
+ * the LDS-table limits -- the interchange pass instead of the gathered loads -- at any N). */
+typedef struct iadmm_lu_ctx iadmm_lu_ctx;
+enum { IADMM_LU_FORCE_HBM = 1 };
+int iadmm_lu_ctx_create(iadmm_lu_ctx** ctx);   /* on the current device; *ctx = NULL on failure */
+int iadmm_lu_ctx_destroy(iadmm_lu_ctx* ctx);   /* waits for the context's streams; NULL is a no-op */
 int64_t iadmm_lu_factor_ws_bytes(int64_t B, int64_t N);
 int iadmm_lu_factor(int64_t B, int64_t N, float* A, int* piv, int* info, void* ws, int64_t ws_bytes,
                     void* stream);
+int iadmm_lu_factor_ex(int64_t B, int64_t N, float* A, int* piv, int* info, void* ws, int64_t ws_bytes,
+                       iadmm_lu_ctx* ctx, int flags, void* stream);
 
 /* Solve with the factors in place (replaces torch.lu_solve, models/lu.py:32,35): x[B,N] holds b
  * on entry and the solution on exit.  x lives in LDS while (N + 4224) floats fit 160 KiB (N <= 36736), in
- * HBM above (several launches per 64-row block); limit N <= 46340. */
+ * HBM above (several launches per 64-row block); limit N <= 46340.  flags (_ex): 0 or IADMM_LU_FORCE_HBM
+ * (the HBM form at any N, tests). */
 int iadmm_lu_solve(int64_t B, int64_t N, const float* LU, const int* piv, float* x, void* stream);
+int iadmm_lu_solve_ex(int64_t B, int64_t N, const float* LU, const int* piv, float* x, int flags, void* stream);
 
 /* Pack the LSTM gate weights for the cell kernel (models/lstm.py:21-38 parameter layout).
  * W_g[2,h], U_g[h,h], b_g[h] for g in (i,f,o,u), W_h[h,1].

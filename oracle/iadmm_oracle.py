@@ -34,7 +34,7 @@ def schedule(params, t, y_like, num_ineq, num_eq):
     [num_ineq, num_ineq+num_eq) get 1e3 * that.
     """
     r = torch.sigmoid(params["rho"][t, :])
-    rv = torch.ones(size=y_like.shape, device=y_like.device) * r
+    rv = torch.ones(size=y_like.shape, device=y_like.device, dtype=y_like.dtype) * r
     lo, hi = num_ineq, num_ineq + num_eq
     rv[:, lo:hi, :] = rv[:, lo:hi, :] * RHO_EQ_OVER_RHO_INEQ
     return rv, 2 * torch.sigmoid(params["alpha"][t, :])
@@ -46,10 +46,10 @@ def kkt_matrix(Q, A0, sigma, rho_vec):
     Bsz, n, _ = Q.shape
     m = A0.shape[1]
     K = torch.empty((Bsz, n + m, n + m), dtype=Q.dtype)
-    K[:, :n, :n] = Q + sigma * torch.diag_embed(torch.ones(size=(Bsz, n)))
+    K[:, :n, :n] = Q + sigma * torch.diag_embed(torch.ones(size=(Bsz, n), dtype=Q.dtype))
     K[:, :n, n:] = A0.permute(0, 2, 1)
     K[:, n:, :n] = A0
-    K[:, n:, n:] = -(1 / rho_vec) * torch.diag_embed(torch.ones(size=(Bsz, m)))
+    K[:, n:, n:] = -(1 / rho_vec) * torch.diag_embed(torch.ones(size=(Bsz, m), dtype=Q.dtype))
     return K
 
 
@@ -129,9 +129,9 @@ def ruiz(Q, p, A0, zl, zu, iters=10):
     """
     Bsz, n, _ = Q.shape
     m = A0.shape[1]
-    eye_n = torch.diag_embed(torch.ones(size=(Bsz, n)))
+    eye_n = torch.diag_embed(torch.ones(size=(Bsz, n), dtype=Q.dtype))
     D = eye_n
-    E = torch.diag_embed(torch.ones(size=(Bsz, m)))
+    E = torch.diag_embed(torch.ones(size=(Bsz, m), dtype=Q.dtype))
     c = 1.0
     for _ in range(iters):
         col_top = torch.max(torch.linalg.norm(Q, ord=torch.inf, dim=1),
@@ -198,11 +198,14 @@ def unscale(sc, x, y, z):
 
 # ----------------------------------------------------------------------------- driver
 def solve(params, Q, p, A0, zl, zu, num_ineq, num_eq, T, sigma, hidden, scaling=True,
-          scaling_iters=10, history=False):
+          scaling_iters=10, history=False, trace=False):
     """Test-mode solve of one batch (main.py:818-1031): scale, T Stage-I iterations, unscale.
 
     Returns a dict with the unscaled final iterate, the scaled state and the final primal/dual
-    residuals on the unscaled data.  ``history=True`` also records per-iteration residuals.
+    residuals on the unscaled data.  ``history=True`` also records per-iteration residuals;
+    ``trace=True`` the unscaled iterate of every iteration (``trace_x/y/z`` [T,B,*,1]).  The
+    arithmetic type is that of the inputs: fp64 data and parameters give the fp64 trajectory the
+    K = 100 envelope test (tests/k100_envelope.py) measures both fp32 paths against.
     """
     Bsz, n, _ = Q.shape
     m = A0.shape[1]
@@ -211,19 +214,24 @@ def solve(params, Q, p, A0, zl, zu, num_ineq, num_eq, T, sigma, hidden, scaling=
     if scaling:
         sc = ruiz(Q, p, A0, zl, zu, scaling_iters)
         Q, p, A0, zl, zu = sc["Q"], sc["p"], sc["A0"], sc["zl"], sc["zu"]
-    x = torch.zeros(Bsz, n, 1)
-    y = torch.zeros(Bsz, m, 1)
-    z = torch.zeros(Bsz, m, 1)
-    xv = torch.zeros(Bsz, n + m, 1)
-    H = torch.zeros(Bsz, n + m, hidden)
-    C = torch.zeros(Bsz, n + m, hidden)
+    dt = dict(dtype=Q.dtype)
+    x = torch.zeros(Bsz, n, 1, **dt)
+    y = torch.zeros(Bsz, m, 1, **dt)
+    z = torch.zeros(Bsz, m, 1, **dt)
+    xv = torch.zeros(Bsz, n + m, 1, **dt)
+    H = torch.zeros(Bsz, n + m, hidden, **dt)
+    C = torch.zeros(Bsz, n + m, hidden, **dt)
     hist = []
+    tr = []
     rho_vec = None
     for t in range(T):
         x, y, z, xv, H, C, _, _, rho_vec = lstm_iteration(params, t, num_ineq, num_eq, x, y, z, xv,
                                                           sigma, H, C, Q, p, A0, zl, zu)
-        if history:
+        if history or trace:
             xs, ys, zs = unscale(sc, x, y, z) if scaling else (x, y, z)
+            if trace:
+                tr.append((xs, ys, zs))
+        if history:
             pr, du, _ = primal_dual(xs, ys, zs, Qu, pu, A0u)
             hist.append((pr.reshape(-1), du.reshape(-1)))
     out = dict(x_scaled=x, y_scaled=y, z_scaled=z, xv=xv, H=H, C=C, rho_vec=rho_vec, scaling=sc)
@@ -234,6 +242,9 @@ def solve(params, Q, p, A0, zl, zu, num_ineq, num_eq, T, sigma, hidden, scaling=
     if history:
         out["hist_primal"] = torch.stack([h[0] for h in hist])
         out["hist_dual"] = torch.stack([h[1] for h in hist])
+    if trace:
+        for i, k in enumerate(("x", "y", "z")):
+            out["trace_" + k] = torch.stack([t[i] for t in tr])
     return out
 
 

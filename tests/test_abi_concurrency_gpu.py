@@ -1,0 +1,152 @@
+"""The C-ABI's stated contract (include/iadmm.h "Conventions"):
+stream-ordered calls that are safe to capture in a hipGraph and to call from several threads on
+distinct streams, and run-to-run determinism of the kernels whose stores go through LDS stages.
+
+* Stage II (models/lu.py:26-35): ``ops.lu_factor`` + ``ops.lu_solve`` captured with
+  ``torch.cuda.graph`` and replayed (the look-ahead context's fork / join across its two streams
+  becomes part of the graph) -- factors, pivots and solutions bitwise those of eager runs;
+* two Python threads factoring different batches on two streams at the same time, each with its own
+  look-ahead context -- bitwise the serial results;
+* the look-ahead (context) path bitwise equal to the single-stream path (NULL context);
+* repeat runs bitwise equal: the LU at N = 2000, B = 4 (look-ahead + LDS-staged panels), and the
+  cell backward (its dP stores staged through LDS, csrc/train.hip) at the config-5 width.
+"""
+import threading
+
+import pytest
+import torch
+
+import iadmm_path  # noqa: F401
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(autouse=True)
+def _gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+
+
+def _kkt_like(B, N, seed):
+    """Random dense matrices with a zero (1,1) entry and a weak diagonal: real interchanges in every
+    block."""
+    g = torch.Generator().manual_seed(seed)
+    K = torch.randn(B, N, N, generator=g)
+    K[:, 0, 0] = 0.0
+    return K.cuda(), torch.randn(B, N, generator=g).cuda()
+
+
+def _factor_solve(K, b, lookahead=True):
+    from iadmm import ops
+    LU, piv, info = ops.lu_factor(K.clone(), lookahead=lookahead)
+    x = ops.lu_solve(LU, piv, b)
+    return LU, piv, info, x
+
+
+def _same(a, b):
+    return all(torch.equal(u, v) for u, v in zip(a, b))
+
+
+@pytest.mark.timeout(300)
+def test_lu_repeat_and_lookahead_bitwise():
+    K, b = _kkt_like(4, 2000, 11)
+    r0 = _factor_solve(K, b)
+    r1 = _factor_solve(K, b)
+    r2 = _factor_solve(K, b, lookahead=False)
+    torch.cuda.synchronize()
+    assert int(r0[2].abs().max()) == 0
+    assert _same(r0, r1), "LU not deterministic across runs"
+    assert _same(r0, r2), "look-ahead path differs from the single-stream path"
+
+
+@pytest.mark.timeout(300)
+def test_lu_graph_capture_replay_bitwise():
+    from iadmm import ops
+    B, N = 4, 2000
+    K, b = _kkt_like(B, N, 12)
+    eager = _factor_solve(K, b)
+    torch.cuda.synchronize()
+    s = torch.cuda.Stream()
+    Ks, bs = K.clone(), b.clone()
+    ws = ops.lu_factor_ws(B, N, K.device)
+    with torch.cuda.stream(s):  # warm-up on the capture stream (makes its look-ahead context)
+        A = Ks.clone()
+        ops.lu_factor(A, ws=ws)
+    s.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=s):
+        A = Ks.clone()
+        LU, piv, info = ops.lu_factor(A, ws=ws)
+        x = ops.lu_solve(LU, piv, bs)
+    Ks.zero_()  # replay must read the current inputs
+    bs.zero_()
+    torch.cuda.synchronize()
+    for _ in range(2):
+        Ks.copy_(K)
+        bs.copy_(b)
+        g.replay()
+        torch.cuda.synchronize()
+        assert _same((LU, piv, info, x), eager), "graph replay differs from eager"
+    # a second input through the same graph
+    K2, b2 = _kkt_like(B, N, 13)
+    ref2 = _factor_solve(K2, b2)
+    Ks.copy_(K2)
+    bs.copy_(b2)
+    g.replay()
+    torch.cuda.synchronize()
+    assert _same((LU, piv, info, x), ref2)
+
+
+@pytest.mark.timeout(300)
+def test_lu_two_threads_two_streams_bitwise():
+    ins = [_kkt_like(8, 2000, 20 + i) for i in range(2)]
+    serial = [_factor_solve(K, b) for K, b in ins]
+    torch.cuda.synchronize()
+    out = [None, None]
+    errs = []
+    start = threading.Barrier(2)
+
+    def work(i):
+        try:
+            s = torch.cuda.Stream()
+            with torch.cuda.stream(s):
+                start.wait()
+                res = [_factor_solve(*ins[i]) for _ in range(3)]
+            s.synchronize()
+            out[i] = res
+        except Exception as e:  # reported below
+            errs.append(e)
+
+    th = [threading.Thread(target=work, args=(i,)) for i in range(2)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=240)
+    assert not errs, errs
+    for i in range(2):
+        for r in out[i]:
+            assert _same(r, serial[i]), f"thread {i} differs from the serial run"
+
+
+@pytest.mark.timeout(300)
+def test_cell_backward_repeat_bitwise():
+    """iadmm_lstm_cell_bwd twice on the same inputs (config-5 micro-batch width: M = 128 x 2000 rows,
+    h = 800): dC, dP (stored through LDS), the W_h slab and the input partials bitwise equal."""
+    from iadmm import data, ops
+    h, M = 800, 128 * 2000
+    p = data.init_lstm_params(h, 100, device="cuda")
+    p = {k: v * 20 for k, v in p.items()}  # larger gates than the 0.01 init: every branch active
+    Upk, Wx = ops.lstm_pack(p, h)
+    g = torch.Generator(device="cuda").manual_seed(5)
+    H = torch.randn(M, h, device="cuda", generator=g)
+    C = torch.randn(M, h, device="cuda", generator=g)
+    xv = torch.randn(M, device="cuda", generator=g)
+    gr = torch.randn(M, device="cuda", generator=g)
+    dq = torch.randn(M, device="cuda", generator=g)
+    dHn = torch.randn(M, h, device="cuda", generator=g)
+    dCn = torch.randn(M, h, device="cuda", generator=g)
+    r0 = ops.lstm_cell_bwd(H, C, xv, gr, Upk, Wx, dq, dHn, dCn)
+    r1 = ops.lstm_cell_bwd(H, C, xv, gr, Upk, Wx, dq, dHn, dCn)
+    torch.cuda.synchronize()
+    assert all(bool(torch.isfinite(t).all()) for t in r0)
+    assert _same(r0, r1), "cell backward not deterministic across runs"

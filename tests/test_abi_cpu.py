@@ -96,11 +96,48 @@ def test_lu_size_limit_is_the_hbm_forms():
         _abi.call("iadmm_lu_solve", 1, 46341, 16, 16, 16, None)
 
 
+def _csrc_without_comments():
+    csrc = os.path.join(REPO, "i-admm-lstm_amd", "csrc")
+    for fn in sorted(os.listdir(csrc)):
+        yield fn, re.sub(r"//[^\n]*|/\*.*?\*/", "", open(os.path.join(csrc, fn)).read(), flags=re.S)
+
+
 def test_no_device_allocation_inside_the_library():
     """Every device buffer is caller-owned: no hipMalloc* / hipFree* call in the HIP sources."""
-    csrc = os.path.join(REPO, "i-admm-lstm_amd", "csrc")
     hits = []
-    for fn in sorted(os.listdir(csrc)):
-        src = re.sub(r"//[^\n]*|/\*.*?\*/", "", open(os.path.join(csrc, fn)).read(), flags=re.S)
+    for fn, src in _csrc_without_comments():
         hits += [f"{fn}: {m.group(0)}" for m in re.finditer(r"\bhip(Malloc|Free)\w*", src)]
     assert not hits, hits
+
+
+def test_no_hidden_state_inside_the_library():
+    """include/iadmm.h's contract: the only HIP objects the library creates are
+    an iadmm_lu_ctx's streams and events, made and destroyed in iadmm_lu_ctx_create / _destroy; no
+    mutex, no function-static or namespace-scope mutable object, no environment read anywhere."""
+    hits = []
+    for fn, src in _csrc_without_comments():
+        for m in re.finditer(r"\bhip(StreamCreate|EventCreate|StreamDestroy|EventDestroy)\w*", src):
+            # the enclosing function: the last extern "C" / static definition before the match
+            head = src[:m.start()]
+            fns = re.findall(r"\b(iadmm_\w+|\w+)\s*\([^;{]*\)\s*\{", head)
+            owner = fns[-1] if fns else "?"
+            if owner not in ("iadmm_lu_ctx_create", "iadmm_lu_ctx_destroy"):
+                hits.append(f"{fn}: {m.group(0)} in {owner}")
+        hits += [f"{fn}: {m.group(0)}" for m in re.finditer(r"\bgetenv\b|std::mutex|\bthread_local\b", src)]
+        hits += [f"{fn}: static local {m.group(0)!r}" for m in
+                 re.finditer(r"\n\s+static\s+(?!constexpr|const\b|inline|__device__|IADMM_DEV|void|int|bool|float)\w[^;(]*;", src)]
+    assert not hits, hits
+
+
+def test_lu_context_abi():
+    """The look-ahead context is created / destroyed through its two calls (no GPU needed to check
+    the argument handling); a NULL context means "everything on the caller's stream"."""
+    lib = _abi.lib()
+    assert lib.iadmm_lu_ctx_destroy(None) == 0
+    with pytest.raises(_abi.IadmmError, match="bad argument"):
+        _abi.call("iadmm_lu_ctx_create", None)
+    need = lib.iadmm_lu_factor_ws_bytes(2, 100)
+    with pytest.raises(_abi.IadmmError, match="bad argument"):  # unknown flag bits
+        _abi.call("iadmm_lu_factor_ex", 2, 100, 16, 16, 16, 16, need, None, 4, None)
+    with pytest.raises(_abi.IadmmError, match="bad argument"):
+        _abi.call("iadmm_lu_solve_ex", 2, 100, 16, 16, 16, 2, None)

@@ -90,7 +90,7 @@ def test_config4_stage2_vs_oracle():
     rows, fails, berr, _ = stage2_envelope.run(st0, cpu, 5, "N=10000")
     assert not fails, fails[:4]
     for b in berr:  # the factorisation itself: no worse than 2x MKL's sgetrf on the same K
-        assert b["hip"]["berr"] <= 2.0 * b["mkl"]["berr"], b
+        assert b["hip"]["berr"] <= 1.5 * b["mkl"]["berr"], b  # r05 two-level U12 (r04: 2.0x, measured 1.33-1.8x)
 
 
 B_FULL = 512

@@ -235,3 +235,44 @@ def test_world4_allreduce_grads_match_to_rounding():
     seen1, _ = _tbptt(_TinySolver(), d, GB, None, chunks=train.global_chunks(GB, 4, MB))
     for a, b in zip(seen[0], seen1[0]):
         assert torch.allclose(a, b, rtol=1e-5, atol=1e-7)
+
+
+def _nograd_worker(rank, world, port, q):
+    """ordered_reduce_grads with a parameter that no micro-batch of any rank touches."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    torch.set_num_threads(1)
+    dist = parallel.init("gloo")
+    from iadmm import train
+    used = torch.nn.Parameter(torch.ones(3))
+    unused = torch.nn.Parameter(torch.ones(2))
+    only_rank1 = torch.nn.Parameter(torch.ones(2))
+    chunks = []
+    for c in range(2):
+        g_used = torch.full((3,), float(1 + c + 10 * rank))
+        g_r1 = torch.full((2,), 5.0) if rank == 1 else None
+        chunks.append([g_used, None, g_r1])
+    train.ordered_reduce_grads([used, unused, only_rank1], chunks, dist)
+    q.put((rank, used.grad.tolist(), unused.grad, only_rank1.grad.tolist() if only_rank1.grad is not None else None))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_ordered_reduce_keeps_none_for_untouched_parameters():
+    """a parameter without a gradient anywhere keeps grad None on every rank (one process
+    leaves it None and Adam skips it); one with a gradient on some rank gets the fold, zeros elsewhere."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_nograd_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=240) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, used, unused, r1 in res:
+        assert used == [1.0 + 2.0 + 11.0 + 12.0] * 3
+        assert unused is None
+        assert r1 == [10.0, 10.0]

@@ -5,7 +5,8 @@ Two forms take over there (csrc/lu.hip): the factorization applies each 128-colu
 interchanges to the columns right of the block in a pass of their own and runs the trailing update
 without gathered loads (its row tables live in LDS, sized for N <= 36736), and the solve keeps x in
 HBM (per 64-row block: one launch for the diagonal triangle, one streaming launch for the rest of
-the vector).  IADMM_LU_FORCE_HBM=1 sends every size through both forms, so they are pinned against
+the vector).  The IADMM_LU_FORCE_HBM flag (iadmm_lu_factor_ex / iadmm_lu_solve_ex) sends every size
+through both forms, so they are pinned against
 the LDS-resident forms at sizes that have both:
 
 * factor: the same arithmetic in the same order, only the interchanges move elsewhere -> the factors
@@ -19,8 +20,6 @@ then N = 36800 (just past the limit) with a planted permutation built on the dev
 (test_stage2_gpu.test_lu_recovers_planted_permutation's construction): partial pivoting must find
 exactly the planted rows, the factors must equal L and U to fp32 accuracy, and the solve of
 b = A x_true must return x_true to fp32 accuracy (cond ~5)."""
-import os
-
 import pytest
 import torch
 
@@ -37,17 +36,10 @@ def _gpu():
 
 def _factor_solve(K, b, force):
     from iadmm import ops
-    old = os.environ.get("IADMM_LU_FORCE_HBM")
-    os.environ["IADMM_LU_FORCE_HBM"] = "1" if force else "0"
-    try:
-        LU, piv, info = ops.lu_factor(K.clone())
-        x = ops.lu_solve(LU, piv, b)
-        torch.cuda.synchronize()
-    finally:
-        if old is None:
-            del os.environ["IADMM_LU_FORCE_HBM"]
-        else:
-            os.environ["IADMM_LU_FORCE_HBM"] = old
+    flags = ops.LU_FORCE_HBM if force else 0
+    LU, piv, info = ops.lu_factor(K.clone(), flags=flags)
+    x = ops.lu_solve(LU, piv, b, flags=flags)
+    torch.cuda.synchronize()
     return LU, piv, info, x
 
 

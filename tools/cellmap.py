@@ -5,7 +5,12 @@ cell_tile_of_block_grouped: row panels per group, hidden tile slowest inside a g
   python tools/cellmap.py [--batch 1024] [--groups 1 2 3 4 5 8] [--reps 5]
 
 Prints one JSON line per group size (mean ms per launch over hipEvents, TF/s against the fp32
-MFMA spec) and checks that every order gives bitwise the same H', C' and projection partials."""
+MFMA spec) and checks that every order gives bitwise the same H', C' and projection partials.
+
+r05: the product library no longer reads IADMM_CELL_PGROUP (include/iadmm.h: no environment reads;
+the study's result, 4 panels per group, is built in).  Rerunning the study needs a variant build
+(tools/build_variant.sh) with the getenv line restored in csrc/lstm.hip; the r02 results are in
+profiles/r02_cellmap_*."""
 import argparse
 import json
 import os

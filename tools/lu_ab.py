@@ -18,7 +18,22 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 def child(args):
     sys.path.insert(0, os.path.join(ROOT, "i-admm-lstm_amd"))
     import torch
-    from iadmm import data, ops
+    from iadmm import _abi, data, ops
+    if getattr(_abi.lib(), "iadmm_lu_factor_ex", None) is None:  # an r04-ABI build (A/B against it)
+        def lu_factor(K, ws=None, **_):
+            B, N = K.shape[0], K.shape[1]
+            piv = torch.empty(B, N, dtype=torch.int32, device=K.device)
+            info = torch.empty(B, dtype=torch.int32, device=K.device)
+            _abi.call("iadmm_lu_factor", B, N, K.data_ptr(), piv.data_ptr(), info.data_ptr(), ws.data_ptr(),
+                      ws.numel() * 4, torch.cuda.current_stream().cuda_stream)
+            return K, piv, info
+
+        def lu_solve(LU, piv, b, **_):
+            x = b.clone()
+            _abi.call("iadmm_lu_solve", LU.shape[0], LU.shape[1], LU.data_ptr(), piv.data_ptr(), x.data_ptr(),
+                      torch.cuda.current_stream().cuda_stream)
+            return x
+        ops.lu_factor, ops.lu_solve = lu_factor, lu_solve
     n = args.N // 2
     mi = me = n // 2
     B = args.batch
