@@ -184,12 +184,31 @@ def box_ceiling(local):
     copy()
     gbs = max(2.0 * nbytes / (copy() * 1e-3) / 1e9 for _ in range(10))
     ok = bool(torch.equal(dst[:1024], src[:1024]))
-    del src, dst, out
+    del dst
+    # r05: a read-only sweep too (the residual matvec is ~all reads; the copy alone measured below the
+    # matvec's own read rate, so it was no ceiling for it): best over workgroups per CU and loads in
+    # flight, 4 GiB (past the 256 MiB Infinity Cache many times over)
+    rbytes = 4 << 30
+    big = torch.ones(rbytes // 4, dtype=torch.float32, device="cuda")
+    rout = torch.empty(32 * cus * 256, dtype=torch.float32, device="cuda")
+    read = {}
+    for wg in (2, 4, 8, 16):
+        for un in (8, 16):
+            fn = lambda: _abi.call("iadmm_probe_read", rbytes, big.data_ptr(), rout.data_ptr(), wg, un,  # noqa: E731
+                                   ops._stream())
+            timed(fn)
+            read[f"{wg}x{un}"] = max(rbytes / (timed(fn) * 1e-3) / 1e9 for _ in range(3))
+    best_read = max(read, key=read.get)
+    del src, big, rout, out
     torch.cuda.empty_cache()
+    hbm = max(gbs, read[best_read])
     return {"mfma_f32_tflops": tflops, "mfma_frac_of_spec": tflops / FP32_MFMA_PEAK_TFLOPS,
-            "hbm_copy_gbs": gbs, "hbm_frac_of_spec": gbs / HBM_PEAK_GBS, "copy_checked": ok,
+            "hbm_copy_gbs": gbs, "hbm_read_gbs": read[best_read], "hbm_read_shape": best_read,
+            "hbm_gbs": hbm, "hbm_frac_of_spec": hbm / HBM_PEAK_GBS, "copy_checked": ok,
             "method": f"csrc/probe.hip: {blocks} x 256-thread workgroups x {it} x 8 register MFMAs "
-                      f"(v_mfma_f32_32x32x2_f32), best of 3; float4 copy of 1 GiB, best of 10; hipEvents"}
+                      f"(v_mfma_f32_32x32x2_f32), best of 3; float4 copy of 1 GiB, best of 10; float4 "
+                      f"read sweep of 4 GiB, best of 3 at each of (workgroups per CU) x (loads in flight) "
+                      f"{sorted(read)}; hbm_gbs = the larger of copy and read; hipEvents"}
 
 
 def baseline_config(args, world):
@@ -576,7 +595,7 @@ def main():
     # per-rank record (which GPU, which instances, how long): gathered to rank 0 (measurement only)
     ranks = parallel.gather_records(dict(rank=rank, first=first, count=count, elapsed_s=elapsed_own,
                                          step_s=step_times, box_mfma_tflops=box["mfma_f32_tflops"],
-                                         box_hbm_gbs=box["hbm_copy_gbs"], **parallel.device_record(local)), dist)
+                                         box_hbm_gbs=box["hbm_gbs"], **parallel.device_record(local)), dist)
 
     res = None
     if rank == 0:
@@ -622,7 +641,7 @@ def main():
         # the same fractions against what this box measured before the timed steps (box_ceiling)
         res["roofline"]["box_ceiling"] = box
         res["roofline"]["frac_vs_box"] = cell_tf / box["mfma_f32_tflops"]
-        res["roofline_matvec"]["frac_vs_box"] = kkt_gbs / box["hbm_copy_gbs"]
+        res["roofline_matvec"]["frac_vs_box"] = kkt_gbs / box["hbm_gbs"]
         per_inst = cell_flop / B * T  # cell flop of one instance's K iterations
         per_gpu = res["value"] / world
         res["step_efficiency"] = {

@@ -1442,6 +1442,12 @@ __global__ __launch_bounds__(NT, NT == 256 ? 4 : (NT == 512 ? 2 : 1)) void lu_so
   for (int i = tid; i < N; i += NT) xb[i] = x[i];
 }
 
+// info[b] = 0 before a factorization (a kernel rather than a memset node: r05)
+__global__ void lu_info_zero_kernel(int64_t B, int* info) {
+  const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (i < B) info[i] = 0;
+}
+
 // b~ = [sigma x - p ; z - y / rho]  (models/lu.py:125,129)
 __global__ void kkt_rhs_kernel(int64_t B, int n, int m, int num_ineq, const float* p, const float* x,
                                const float* y, const float* z, float sigma, const float* scal,
@@ -1657,13 +1663,16 @@ static int lu_factor_blocks(int64_t B, int64_t N, float* A, int* piv, int* info,
   const bool defer = gather && N <= kLeftDeferMaxN;
   const int nb = (int)((N + kOB - 1) / kOB);
   const int64_t slot = B * (int64_t)kPermInts;
-  // look-ahead (with defer): block t's trailing update is two launches -- strip 0 (block t + 1's own
-  // columns) on s, the other strips on a side stream -- so that block t + 1's panels, interchanges,
-  // in-block updates and L11^-1, which touch only block t + 1's columns once the left interchanges
-  // are deferred, run beside the rest of block t's update; block t + 1's trailing update waits for
-  // it.  L11^-1 alternates between two buffers (the side launch of block t still reads its own).
-  // (without a context, or above N = 2048, everything runs in order on the caller's stream)
-  iadmm_lu_ctx* side = defer ? ctx : nullptr;
+  // look-ahead (with a context): block t's trailing update is two launches -- strip 0 (block t + 1's
+  // own columns) on s, the other strips on a side stream -- so that block t + 1's panels, in-block
+  // interchanges, in-block updates and L11^-1, which touch only block t + 1's columns, run beside the
+  // rest of block t's update; block t + 1's trailing update waits for it.  The one step of block t + 1
+  // that reaches further left -- its interchanges on the columns [0, P), which hold block t's L21 that
+  // the side launch still reads -- waits for it too (N > 2048, r05; N <= 2048 defers that step to the
+  // end).  L11^-1 and (without defer) the block permutation alternate between two buffers.
+  // (without a context, or with the interchanges as a pass of their own (gather = false), everything
+  // runs in order on the caller's stream)
+  iadmm_lu_ctx* side = gather ? ctx : nullptr;
   if (side) {
     // Under stream capture every launch stays on the caller's stream (same factors, bit for bit):
     // capturing the fork / join across the context's two streams crashed the HIP 7.2 runtime in
@@ -1689,7 +1698,7 @@ static int lu_factor_blocks(int64_t B, int64_t N, float* A, int* piv, int* info,
   for (int P = 0; P < N && !rc; P += kOB) {
     const int n_ = (int)N;
     const int c1 = std::min(n_, P + kBlk), c2 = std::min(n_, P + kOB);
-    int* pm = defer ? perm + (P / kOB) * slot : perm;
+    int* pm = defer ? perm + (P / kOB) * slot : (side ? perm + ((P / kOB) & 1) * slot : perm);
     // first half: factor; its interchanges and U12 on the second half's columns only, then the second
     // half's rank-64 update
     rc = lu_factor_half(B, N, P, c1, A, piv, info, s);
@@ -1708,6 +1717,10 @@ static int lu_factor_blocks(int64_t B, int64_t N, float* A, int* piv, int* info,
     if (!perm_in_linv) {
       hipLaunchKernelGGL(lu_block_perm_kernel, dim3((unsigned)B), dim3(64), 0, s, (int)N, P, c2, piv, pm);
       LU_TRY_LAUNCH();
+    }
+    if (!defer && pending) {  // block t - 1's other strips read its L21, which the left interchanges move
+      LU_TRY(hipStreamWaitEvent(s, side->join, 0));
+      pending = false;
     }
     rc = lu_swap(B, N, P, c2, 0, defer ? 0 : P, gather ? 0 : c2, gather ? 0 : n_, 0, A, piv, pm, s, false);
     if (rc || c2 >= n_) break;
@@ -1893,19 +1906,20 @@ static int lu_solve_hbm(int64_t B, int64_t N, const float* LU, const int* piv, f
 }
 
 // workspace: per-instance block permutations (kPermInts ints; N <= kLeftDeferMaxN: one slot per
-// 128-column block, then the deferred left interchanges' sigma tables), then the 128 x 128 L11^-1 of
-// the current outer block (each part 16-B aligned)
+// 128-column block, then the deferred left interchanges' sigma tables; up to kLuMaxN two alternating
+// slots), then the 128 x 128 two-level L11^-1 of the current outer block (two alternating buffers up
+// to kLuMaxN; each part 16-B aligned)
 static int64_t al16(int64_t n) { return (n + 15) / 16 * 16; }
 static int64_t lu_nb(int64_t N) { return (N + kOB - 1) / kOB; }
-static int64_t lu_perm_bytes(int64_t B, int64_t N) {
-  return al16(B * (int64_t)kPermInts * (N <= kLeftDeferMaxN ? lu_nb(N) : 1) * (int64_t)sizeof(int));
+static int64_t lu_perm_bytes(int64_t B, int64_t N) {  // (two alternating slots for the look-ahead)
+  return al16(B * (int64_t)kPermInts * (N <= kLeftDeferMaxN ? lu_nb(N) : (N <= kLuMaxN ? 2 : 1)) * (int64_t)sizeof(int));
 }
 static int64_t lu_sig_bytes(int64_t B, int64_t N) {
   return N <= kLeftDeferMaxN ? al16(B * left_sig_off(N, lu_nb(N) - 1) * (int64_t)sizeof(int)) : 0;
 }
 static int64_t lu_ws_bytes(int64_t B, int64_t N) {  // (two L11^-1 buffers with the look-ahead)
   return lu_perm_bytes(B, N) + lu_sig_bytes(B, N) +
-         (N <= kLeftDeferMaxN ? 2 : 1) * B * (int64_t)kLinvFloats * (int64_t)sizeof(float);
+         (N <= kLuMaxN ? 2 : 1) * B * (int64_t)kLinvFloats * (int64_t)sizeof(float);
 }
 
 extern "C" int64_t iadmm_lu_factor_ws_bytes(int64_t B, int64_t N) {
@@ -1961,8 +1975,8 @@ extern "C" int iadmm_lu_factor_ex(int64_t B, int64_t N, float* A, int* piv, int*
     if (dev != ctx->device) return IADMM_E_ARG;
   }
   hipStream_t s = (hipStream_t)stream;
-  const hipError_t e = hipMemsetAsync(info, 0, B * sizeof(int), s);
-  if (e != hipSuccess) return (int)e;
+  hipLaunchKernelGGL(lu_info_zero_kernel, dim3((unsigned)((B + 255) / 256)), dim3(256), 0, s, B, info);
+  IADMM_CHECK_LAUNCH();
   int* perm = static_cast<int*>(ws);
   int* sig = reinterpret_cast<int*>(static_cast<char*>(ws) + lu_perm_bytes(B, N));
   float* linv = reinterpret_cast<float*>(static_cast<char*>(ws) + lu_perm_bytes(B, N) + lu_sig_bytes(B, N));

@@ -7,6 +7,10 @@
 //                      from registers (no memory in the loop): 4096 flop per MFMA per wave; two
 //                      4-wave workgroups per CU = 2 waves per SIMD, the cell kernel's residency.
 //   probe_copy_kernel  float4 copy, one contiguous chunk per workgroup (16-B accesses, 8 in flight per thread).
+//   probe_read_kernel  float4 read-only sweep (the residual matvec's access: 16-B loads, one contiguous
+//                      chunk per workgroup), UNROLL loads in flight per thread, at a chosen number of
+//                      workgroups per CU (r05: the copy alone, 5.3 TB/s, sat below the matvec's own
+//                      5.65 TB/s of reads, so it was no ceiling for it; bench.py takes the best shape).
 #include <algorithm>
 
 #include "common.h"
@@ -52,6 +56,25 @@ __global__ __launch_bounds__(256) void probe_copy_kernel(int64_t n4, const float
   for (; i < c1; i += 256) dst[i] = src[i];
 }
 
+template <int UNROLL>
+__global__ __launch_bounds__(256) void probe_read_kernel(int64_t n4, const float4* __restrict__ src, float* out) {
+  const int64_t per = (n4 + gridDim.x - 1) / gridDim.x;
+  const int64_t c0 = (int64_t)blockIdx.x * per, c1 = c0 + per < n4 ? c0 + per : n4;
+  typedef float f4v __attribute__((ext_vector_type(4)));
+  const f4v* s4 = reinterpret_cast<const f4v*>(src);
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  int64_t i = c0 + threadIdx.x;
+  for (; i + (UNROLL - 1) * 256 < c1; i += UNROLL * 256) {
+    f4v v[UNROLL];
+#pragma unroll
+    for (int u = 0; u < UNROLL; ++u) v[u] = __builtin_nontemporal_load(s4 + i + u * 256);
+#pragma unroll
+    for (int u = 0; u < UNROLL; ++u) { acc.x += v[u].x; acc.y += v[u].y; acc.z += v[u].z; acc.w += v[u].w; }
+  }
+  for (; i < c1; i += 256) { const float4 v = src[i]; acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w; }
+  out[(size_t)blockIdx.x * blockDim.x + threadIdx.x] = (acc.x + acc.y) + (acc.z + acc.w);
+}
+
 }  // namespace iadmm
 
 using namespace iadmm;
@@ -77,5 +100,23 @@ extern "C" int iadmm_probe_copy(int64_t bytes, const void* src, void* dst, void*
   const int64_t blocks = std::min<int64_t>((n4 + 255) / 256, (int64_t)cus * 8);
   hipLaunchKernelGGL(probe_copy_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, n4,
                      static_cast<const float4*>(src), static_cast<float4*>(dst));
+  return (int)hipGetLastError();
+}
+
+extern "C" int iadmm_probe_read(int64_t bytes, const void* src, float* out, int64_t wg_per_cu, int64_t unroll,
+                                void* stream) {
+  if (bytes <= 0 || !src || !out || wg_per_cu <= 0 || wg_per_cu > 32 || (unroll != 8 && unroll != 16))
+    return IADMM_E_ARG;
+  if ((bytes & 15) || (reinterpret_cast<uintptr_t>(src) & 15)) return IADMM_E_ALIGN;
+  int dev = 0, cus = 256;
+  (void)hipGetDevice(&dev);
+  (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  const int64_t n4 = bytes / 16, blocks = (int64_t)cus * wg_per_cu;
+  if (unroll == 8)
+    hipLaunchKernelGGL(probe_read_kernel<8>, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, n4,
+                       static_cast<const float4*>(src), out);
+  else
+    hipLaunchKernelGGL(probe_read_kernel<16>, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, n4,
+                       static_cast<const float4*>(src), out);
   return (int)hipGetLastError();
 }

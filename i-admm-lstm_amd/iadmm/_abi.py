@@ -70,6 +70,7 @@ SIGNATURES = {
     "iadmm_probe_mfma_flop": (i64, [i64, i64]),
     "iadmm_probe_mfma": (cint, [i64, i64, vp, vp]),
     "iadmm_probe_copy": (cint, [i64, vp, vp, vp]),
+    "iadmm_probe_read": (cint, [i64, vp, vp, i64, i64, vp]),
 }
 
 ERRORS = {-1: "bad argument", -2: "size beyond kernel limit", -3: "misaligned pointer"}

@@ -120,15 +120,16 @@ int iadmm_kkt_rhs(int64_t B, int64_t n, int64_t m, int64_t num_ineq, const float
  * N <= 2048 (r04): the interchanges left of each block are applied once at the end.
  * ws: caller-owned, 16-B aligned device workspace of at least iadmm_lu_factor_ws_bytes(B, N) bytes
  * (per-instance block permutations -- one per 128-column block for N <= 2048, with the composed
- * left permutations -- and the 128x128 L11^-1 blocks, two for N <= 2048); nothing is allocated inside.
- * iadmm_lu_factor runs every launch in order on `stream`.  iadmm_lu_factor_ex with a context (N <= 2048)
+ * left permutations, two for N <= 36736 -- and the 128x128 two-level L11^-1 blocks, two for N <= 36736);
+ * nothing is allocated inside.
+ * iadmm_lu_factor runs every launch in order on `stream`.  iadmm_lu_factor_ex with a context (N <= 36736)
  * factors the next block beside the rest of each trailing update (look-ahead) on the context's two
  * streams (high / low priority), forked from and joined back into `stream` on every path, errors
  * included: the call stays asynchronous and ordered on `stream`, and the factors are bit for bit
- * those of iadmm_lu_factor.  Under stream capture (hipGraph) the call ignores the context and runs every
- * launch on `stream` (the cross-stream fork / join crashed the HIP 7.2 runtime at capture end).  A context belongs to the device current at its creation (IADMM_E_ARG
- * on another) and serves one factorization at a time in its streams' order: give each concurrent
- * caller (thread / stream) its own.  flags: 0, or IADMM_LU_FORCE_HBM (tests: the forms for N above
+ * those of iadmm_lu_factor.  Under stream capture (hipGraph) the call ignores the context and runs
+ * every launch on `stream` (the cross-stream fork / join crashed the HIP 7.2 runtime at capture end).
+ * A context belongs to the device current at its creation (IADMM_E_ARG on another) and serves one
+ * factorization at a time in its streams' order: give each concurrent caller (thread / stream) its own.  flags: 0, or IADMM_LU_FORCE_HBM (tests: the forms for N above
  * the LDS-table limits -- the interchange pass instead of the gathered loads -- at any N). */
 typedef struct iadmm_lu_ctx iadmm_lu_ctx;
 enum { IADMM_LU_FORCE_HBM = 1 };
@@ -342,10 +343,14 @@ int iadmm_loss_grad_split(int64_t B, int64_t n, int64_t m, const float* Q, const
  *     v_mfma_f32_32x32x2_f32 from registers; iadmm_probe_mfma_flop(blocks, iters) flop in all;
  *     out[blocks*256] receives per-thread sums (keeps the MFMAs live).
  *   iadmm_probe_copy: float4 copy of ``bytes`` (multiple of 16, 16-B aligned src/dst): 2*bytes of
- *     HBM traffic. */
+ *     HBM traffic.
+ *   iadmm_probe_read: float4 read-only sweep of ``bytes`` by wg_per_cu (1..32) x CUs workgroups of 256
+ *     threads, ``unroll`` (8 or 16) loads in flight per thread; out[wg_per_cu * CUs * 256] gets the
+ *     per-thread sums (keeps the loads live). */
 int64_t iadmm_probe_mfma_flop(int64_t blocks, int64_t iters);
 int iadmm_probe_mfma(int64_t blocks, int64_t iters, float* out, void* stream);
 int iadmm_probe_copy(int64_t bytes, const void* src, void* dst, void* stream);
+int iadmm_probe_read(int64_t bytes, const void* src, float* out, int64_t wg_per_cu, int64_t unroll, void* stream);
 
 #ifdef __cplusplus
 }

@@ -47,6 +47,17 @@ def _same(a, b):
     return all(torch.equal(u, v) for u, v in zip(a, b))
 
 
+def _diff(a, b):
+    """Which of (LU, piv, info, x) differ, and by how much (for the failure message)."""
+    out = {}
+    for name, u, v in zip(("LU", "piv", "info", "x"), a, b):
+        if not torch.equal(u, v):
+            ne = (u != v)
+            out[name] = (int(ne.sum()), float((u.double() - v.double()).abs().max()),
+                         tuple(int(i) for i in ne.nonzero()[0].tolist()))
+    return out
+
+
 @pytest.mark.timeout(300)
 def test_lu_repeat_and_lookahead_bitwise():
     K, b = _kkt_like(4, 2000, 11)
@@ -55,8 +66,8 @@ def test_lu_repeat_and_lookahead_bitwise():
     r2 = _factor_solve(K, b, lookahead=False)
     torch.cuda.synchronize()
     assert int(r0[2].abs().max()) == 0
-    assert _same(r0, r1), "LU not deterministic across runs"
-    assert _same(r0, r2), "look-ahead path differs from the single-stream path"
+    assert _same(r0, r1), ("LU not deterministic across runs", _diff(r0, r1))
+    assert _same(r0, r2), ("look-ahead path differs from the single-stream path", _diff(r0, r2))
 
 
 @pytest.mark.timeout(300)
@@ -86,7 +97,7 @@ def test_lu_graph_capture_replay_bitwise():
         bs.copy_(b)
         g.replay()
         torch.cuda.synchronize()
-        assert _same((LU, piv, info, x), eager), "graph replay differs from eager"
+        assert _same((LU, piv, info, x), eager), ("graph replay differs from eager", _diff((LU, piv, info, x), eager))
     # a second input through the same graph
     K2, b2 = _kkt_like(B, N, 13)
     ref2 = _factor_solve(K2, b2)
@@ -94,7 +105,7 @@ def test_lu_graph_capture_replay_bitwise():
     bs.copy_(b2)
     g.replay()
     torch.cuda.synchronize()
-    assert _same((LU, piv, info, x), ref2)
+    assert _same((LU, piv, info, x), ref2), _diff((LU, piv, info, x), ref2)
 
 
 @pytest.mark.timeout(300)

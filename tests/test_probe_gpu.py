@@ -18,6 +18,8 @@ def test_box_ceiling_rates_are_plausible():
     assert box["copy_checked"]
     assert 0.5 * bench.FP32_MFMA_PEAK_TFLOPS < box["mfma_f32_tflops"] < 1.02 * bench.FP32_MFMA_PEAK_TFLOPS
     assert 0.4 * bench.HBM_PEAK_GBS < box["hbm_copy_gbs"] < 1.0 * bench.HBM_PEAK_GBS
+    assert 0.4 * bench.HBM_PEAK_GBS < box["hbm_read_gbs"] < 1.0 * bench.HBM_PEAK_GBS
+    assert box["hbm_gbs"] == max(box["hbm_copy_gbs"], box["hbm_read_gbs"])
 
 
 def test_probe_arguments_rejected():
@@ -29,3 +31,6 @@ def test_probe_arguments_rejected():
     assert L.iadmm_probe_mfma(0, 10, x.data_ptr(), None) == -1
     assert L.iadmm_probe_copy(12, x.data_ptr(), x.data_ptr(), None) == -3
     assert L.iadmm_probe_copy(16, None, x.data_ptr(), None) == -1
+    assert L.iadmm_probe_read(16, x.data_ptr(), x.data_ptr(), 0, 8, None) == -1
+    assert L.iadmm_probe_read(16, x.data_ptr(), x.data_ptr(), 4, 4, None) == -1
+    assert L.iadmm_probe_read(12, x.data_ptr(), x.data_ptr(), 4, 8, None) == -3

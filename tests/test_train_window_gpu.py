@@ -12,7 +12,10 @@ parameter (stated before measuring):
     rel-L2(grad_HIP - grad_fp64) <= 2 x rel-L2(grad_fp32 oracle - grad_fp64) + 1e-7.
 
 Two weight sets: the reference's initialisation (models/lstm.py:21-41, seed 17) and the same
-weights x 20 (gates away from their linear regime, larger rho / alpha excursions).
+weights x 6 (gates away from their linear regime, larger rho / alpha excursions).  (r05 first tried
+x 20: that drives the solve into a chaotic regime -- loss 4e4 -- where the fp32 oracle's gradient is
+2.5e-3 from fp64 on the GPU's instances and 1.6 (i.e. uncorrelated) on the CPU generator's, and any two
+fp32 orders of the same algorithm disagree by that much: a coin toss, not a test of the kernels.)
 """
 import os
 
@@ -52,7 +55,7 @@ def oracle_grads(params, d, dtype):
 
 
 @pytest.mark.timeout(600)
-@pytest.mark.parametrize("scale", [1.0, 20.0])
+@pytest.mark.parametrize("scale", [1.0, 6.0])
 def test_full_window_grads_fp64_envelope(scale):
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
