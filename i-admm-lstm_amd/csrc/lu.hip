@@ -119,28 +119,34 @@ constexpr size_t trail_lds() { return ((size_t)(TCW + kTRS) * kTS + 2 * (size_t)
 constexpr size_t kTrailLds = trail_lds<kTC>();
 
 // The net row permutation of n interchanges (row base + j <-> pv[j], in order, ?laswp):
-// afterwards row rowid[i] holds what row cur[i] held before, for i < *cnt (<= 2n <= 256; rowid[i] =
-// base + i for i < n).  Built by wave 0 with both lists in registers (entry i = lane i % 64 of slot
+// afterwards row rowid[i] holds what row cur[i] held before, for i < *cnt (<= 2n <= 64 NS; rowid[i] =
+// base + i for i < n).  Built by one wave with both lists in registers (entry i = lane i % 64 of slot
 // i / 64): per interchange a ballot search over the live slots and lane-indexed reads and writes,
 // no LDS round trip (r04: the LDS-resident lists cost ~500 cycles per interchange, ~30 us for a
 // 128-row block); the lists go to LDS once at the end.  The caller moves each column with all loads
-// before all stores, one memory latency instead of n.
+// before all stores, one memory latency instead of n.  NS = 4: a block (n <= 128); NS = 8: a pair of
+// blocks (n <= 256, r05 lu_pair_perm_kernel).
 // (wave: the wave that builds; sync = false: no closing barrier -- only that wave reads the lists)
+template <int NS = 4>
 IADMM_DEV void build_row_perm(const int* pv, int base, int n, int* rowid, int* cur, int* cnt, int wave = 0,
                               bool sync = true) {
   const int lane = threadIdx.x & 63;
   if ((int)(threadIdx.x >> 6) == wave) {
-    int rw[4], cr[4];
+    int rw[NS], cr[NS], pvr[NS / 2];
 #pragma unroll
-    for (int s = 0; s < 4; ++s) rw[s] = cr[s] = base + 64 * s + lane;
-    const int pv0 = pv[min(lane, n - 1)], pv1 = pv[min(64 + lane, n - 1)];
+    for (int s = 0; s < NS; ++s) rw[s] = cr[s] = base + 64 * s + lane;
+#pragma unroll
+    for (int s = 0; s < NS / 2; ++s) pvr[s] = pv[min(64 * s + lane, n - 1)];
     int c = n;
     for (int j = 0; j < n; ++j) {
-      const int p = __builtin_amdgcn_readlane(j < 64 ? pv0 : pv1, j & 63);
+      int pj = pvr[0];
+#pragma unroll
+      for (int s = 1; s < NS / 2; ++s) pj = s == (j >> 6) ? pvr[s] : pj;
+      const int p = __builtin_amdgcn_readlane(pj, j & 63);
       if (p == base + j) continue;
       int found = -1;
 #pragma unroll
-      for (int s = 0; s < 4; ++s) {
+      for (int s = 0; s < NS; ++s) {
         if (found < 0 && 64 * s < c) {
           const unsigned long long m = __ballot(rw[s] == p && 64 * s + lane < c);
           if (m) found = 64 * s + __ffsll((long long)m) - 1;
@@ -149,21 +155,25 @@ IADMM_DEV void build_row_perm(const int* pv, int base, int n, int* rowid, int* c
       if (found < 0) {
         found = c++;
 #pragma unroll
-        for (int s = 0; s < 4; ++s)
+        for (int s = 0; s < NS; ++s)
           if (s == (found >> 6) && lane == (found & 63)) { rw[s] = p; cr[s] = p; }
       }
       const int sj = j >> 6, sf = found >> 6;
-      const int vj = sj == 0 ? cr[0] : (sj == 1 ? cr[1] : (sj == 2 ? cr[2] : cr[3]));
-      const int vf = sf == 0 ? cr[0] : (sf == 1 ? cr[1] : (sf == 2 ? cr[2] : cr[3]));
+      int vj = cr[0], vf = cr[0];  // cr[sj], cr[sf] for wave-uniform run-time slots (registers only)
+#pragma unroll
+      for (int s = 1; s < NS; ++s) {
+        vj = s == sj ? cr[s] : vj;
+        vf = s == sf ? cr[s] : vf;
+      }
       const int tj = __builtin_amdgcn_readlane(vj, j & 63), tf = __builtin_amdgcn_readlane(vf, found & 63);
 #pragma unroll
-      for (int s = 0; s < 4; ++s) {
+      for (int s = 0; s < NS; ++s) {
         if (s == sj && lane == (j & 63)) cr[s] = tf;
         if (s == sf && lane == (found & 63)) cr[s] = tj;
       }
     }
 #pragma unroll
-    for (int s = 0; s < 4; ++s)
+    for (int s = 0; s < NS; ++s)
       if (64 * s + lane < c) { rowid[64 * s + lane] = rw[s]; cur[64 * s + lane] = cr[s]; }
     if (lane == 0) *cnt = c;
   }
@@ -938,7 +948,7 @@ static_assert(2 * kT2Lds <= 160 * 1024, "two workgroups per CU (gfx950 LDS)");
 constexpr int kLinvFloats = kOB * kOB;
 
 // Two-level L11^-1 of the block's 128 x 128 unit-lower factor (r05), row-major 128 x 128 into Linv[b]:
-// the four 32 x 32 diagonal blocks inverted (Linv_jj), the blocks below them as -L_ij, zeros above.
+// the four 32 x 32 diagonal blocks inverted (Linv_jj), the blocks below them as L_ij, zeros above.
 // lu_trail128_kernel's prologue then forms U12 block row by block row, U_j = Linv_jj (A_j - sum_{i<j}
 // L_ji U_i): substitution between the 32-row blocks, explicit inverses only within them.  (r04: the
 // explicit inverse of the whole 128 x 128 factor; its residual grows with kappa(L11) where
@@ -1001,7 +1011,7 @@ __global__ __launch_bounds__(kOB + 64) void lu_linv_kernel(int N, int P, const f
 #pragma unroll
     for (int t = 0; t < kLd; ++t) {
       const int i = bi * kLd + t;
-      out[i * kOB + j] = kLd * bi == d0 ? x[t] : (kLd * bi > d0 ? -L[i][j] : 0.f);
+      out[i * kOB + j] = kLd * bi == d0 ? x[t] : (kLd * bi > d0 ? L[i][j] : 0.f);
     }
 }
 
@@ -1093,8 +1103,9 @@ __global__ __launch_bounds__(kT2Threads, 2) void lu_trail128_kernel(int N, int P
   // (published by the prologue's barriers)
 
   // ---- prologue (r05, two-level): U12 = L11^-1 A12 on this strip by 32-row blocks,
-  // U_j = Linv_jj (A_j - sum_{i<j} L_ji U_i) (lu_linv_kernel's layout: Linv_jj on the diagonal, -L_ji
-  // below).  Wave w owns the strip's columns [32w, 32w + 32) for all 128 rows, so it needs no other
+  // U_j = Linv_jj (A_j - sum_{i<j} L_ji U_i) (lu_linv_kernel's layout: Linv_jj on the diagonal, L_ji
+  // below), carried negated -- acc = -A_j + sum L_ji U_i, U_j = -(Linv_jj acc), exact sign flips, so
+  // no operand needs negating (and lu_trail256_kernel can stage L rows straight from A by LDS-DMA).  Wave w owns the strip's columns [32w, 32w + 32) for all 128 rows, so it needs no other
   // wave's result: its U_i are accumulator tiles (lane half h: rows 8q + 4h + r of the block, column
   // il), and the MFMA k index runs over exactly those rows -- U_i is the B operand straight from
   // registers, the matching L entries (four consecutive k) one 16-B LDS read.  A_j is the first
@@ -1127,7 +1138,7 @@ __global__ __launch_bounds__(kT2Threads, 2) void lu_trail128_kernel(int N, int P
   __syncthreads();  // Lt staged
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
-    floatx16 acc = u[j];
+    floatx16 acc = -u[j];
 #pragma unroll
     for (int i = 0; i < j; ++i)
 #pragma unroll
@@ -1145,7 +1156,7 @@ __global__ __launch_bounds__(kT2Threads, 2) void lu_trail128_kernel(int N, int P
       for (int r = 0; r < 4; ++r)
         o = __builtin_amdgcn_mfma_f32_32x32x2f32(get4(l4, r), acc[4 * q + r], (q == 0 && r == 0) ? zero : o, 0, 0, 0);
     }
-    u[j] = o;
+    u[j] = -o;
   }
   __syncthreads();  // the pass tiles consumed: U12^T over them
   // accumulator v of tile j <-> U12 row 32j + 8(v/4) + 4h + v%4, strip column 32w + il
@@ -1309,6 +1320,318 @@ __global__ __launch_bounds__(kT2Threads, 2) void lu_trail128_kernel(int N, int P
 #pragma unroll
     for (int sg = 0; sg < kOB / 8; ++sg) {
       const int i = (kOB / 2) * h + 4 * sg;
+      float* dst = Ab + (size_t)(P + i) * N + cb + wc + il;
+      dst[0] = ub[sg].x;
+      dst[(size_t)N] = ub[sg].y;
+      dst[2 * (size_t)N] = ub[sg].z;
+      dst[3 * (size_t)N] = ub[sg].w;
+    }
+  }
+}
+
+// ---- Paired blocks (r05): one rank-256 update of the far columns per two 128-column blocks ----
+// At rank 128 the trailing update streams A22 at 32 flop/B: 157 TF/s of fp32 MFMA would need ~9.8 TB/s
+// of HBM for A22 alone, so lu_trail128_kernel is memory-bound (~0.6 of MFMA).  With the left
+// interchanges deferred (N <= 2048), blocks t (even) and t + 1 are factored back to back -- block t
+// updating only block t + 1's columns (lu_trail128_kernel, strip 0) -- and everything right of block
+// t + 1 then gets ONE update with both blocks' factors:
+//   U12 = L^-1 A12 over the pair's 256 rows (two-level: 32-row blocks, Linv_jj from each block's
+//         lu_linv_kernel buffer; L = [[L11_t, 0], [L_{t+1,t}, L11_{t+1}]], L_{t+1,t} = block t's
+//         multipliers in block t + 1's rows);
+//   A22 -= [L21_t  L21_{t+1}] U12   (rank 256: 64 flop/B, MFMA-bound).
+// Interchanges: the far columns have had neither block's applied -- A22 and A12 rows gather through the
+// pair's composed permutation (lu_pair_perm_kernel: the pair's 256 pivots in order); block t's columns
+// have had block t + 1's interchanges deferred too, so L21_t rows gather through block t + 1's own
+// permutation.  A displaced row's source is always one of the pair's 256 block rows, which take U12
+// only after the last step's loads (as in lu_trail128_kernel).
+constexpr int kR2 = 2 * kOB;                 // rank of the paired update
+constexpr int kP2K = kR2 + 4;                // LDS stride (k) of its L21 tiles, staged L rows and U12^T
+constexpr int kPairMax = kR2;                // interchanges of a pair
+constexpr int kPairInts = 4 * kPairMax + 1;  // rowid[512], cur[512], cnt
+constexpr int kP2BitWords = (2048 + kT2S - 1) / kT2S + 2;  // (pairing only with the deferred left pass)
+constexpr int kP2MainFloats = 2 * kT2S * kP2K + 2 * kT2S * kT2CS;
+constexpr int kP2ProFloats = kOB * kP2K;
+constexpr int kP2AreaFloats = kP2MainFloats > kP2ProFloats ? kP2MainFloats : kP2ProFloats;
+constexpr size_t kP2Lds = (size_t)kP2AreaFloats * sizeof(float) +
+                          (size_t)(4 * kPairMax + 3 * kPermMax + 2 * kP2BitWords) * sizeof(int) +
+                          2 * (size_t)((kP2BitWords + 3) & ~3);
+static_assert(kP2Lds <= 160 * 1024, "one workgroup per CU (gfx950 LDS)");
+
+// one wave per instance: the composed permutation of the pair's 256 interchanges (rows [P, P + 256))
+__global__ __launch_bounds__(64) void lu_pair_perm_kernel(int N, int P, const int* piv, int* pperm) {
+  __shared__ int pvs[kPairMax], prow[2 * kPairMax], pcur[2 * kPairMax], pcnt[1];
+  const int lane = threadIdx.x;
+  const size_t b = blockIdx.x;
+  for (int i = lane; i < kPairMax; i += 64) pvs[i] = piv[b * N + P + i] - 1;
+  __syncthreads();
+  build_row_perm<8>(pvs, P, kPairMax, prow, pcur, pcnt, 0, false);
+  int* out = pperm + b * kPairInts;
+  const int cnt = *pcnt;
+  for (int i = lane; i < 2 * kPairMax; i += 64) { out[i] = i < cnt ? prow[i] : 0; out[2 * kPairMax + i] = i < cnt ? pcur[i] : 0; }
+  if (lane == 0) out[4 * kPairMax] = cnt;
+}
+
+// The paired far update: per (instance, 128-column strip right of the pair), all rows below it.  Four
+// waves, ONE workgroup per CU (140 KB of LDS; up to 512 registers per wave: the U12 operand alone is
+// 128 per lane at rank 256).  Same step structure as lu_trail128_kernel (32-row steps, L21 and the
+// product double-buffered in LDS, one barrier per step, row-contiguous 16-B A22 accesses) with
+// 128 MFMAs per wave and step.  N % 4 == 0, 16-B aligned rows, N <= 2048 (the host checks).
+// Linv0 / Linv1: the two blocks' lu_linv_kernel buffers; pperm: the pair's composed permutation;
+// perm1: block t + 1's own permutation (lu_linv_kernel's perm wave).
+__global__ __launch_bounds__(kT2Threads, 1) void lu_trail256_kernel(int N, int P, int ntc, int tc0, float* A,
+                                                                    const float* Linv0, const float* Linv1,
+                                                                    const int* pperm, const int* perm1) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  float* Ls0 = sm;                       // 2 x [32 rows][kP2K]: L21 of a step (k < 128: block t)
+  float* Cb0 = sm + 2 * kT2S * kP2K;     // 2 x [32 rows][kT2CS]: product of a step
+  float* Lt = sm;                        // prologue: staged L rows [128][kP2K]
+  float* Ut = sm;                        // then U12^T [128 cols][kP2K]
+  int* bsrc = reinterpret_cast<int*>(sm + kP2AreaFloats);  // [256] source row of pair row P + i
+  int* tdst = bsrc + kPairMax;           // [256] displaced rows (composed) and
+  int* tsrc = tdst + kPairMax;           // [256] their sources, as given;
+  int* dsrc = tsrc + kPairMax;           // [256] the sources sorted by displaced row
+  int* tdst1 = dsrc + kPairMax;          // [128] block t + 1's displaced rows,
+  int* tsrc1 = tdst1 + kPermMax;         // [128] their sources,
+  int* dsrc1 = tsrc1 + kPermMax;         // [128] sorted
+  unsigned* dbits = reinterpret_cast<unsigned*>(dsrc1 + kPermMax);
+  unsigned* dbits1 = dbits + kP2BitWords;
+  unsigned char* dpre = reinterpret_cast<unsigned char*>(dbits1 + kP2BitWords);
+  unsigned char* dpre1 = dpre + ((kP2BitWords + 3) & ~3);
+  const int nwg = gridDim.x, bid = blockIdx.x;
+  const int xcd = bid & 7, local = bid >> 3, q8 = nwg >> 3, r8 = nwg & 7;
+  const int logical = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + local;
+  const size_t b = (size_t)(logical / ntc);
+  const int tc = tc0 + logical % ntc;
+  float* Ab = A + b * (size_t)N * N;
+  const int P1 = P + kOB, c0 = P + kR2, cb = c0 + tc * kT2C;
+  const int nsteps = (N - c0 + kT2S - 1) / kT2S;
+  const int tid = threadIdx.x, lane = tid & 63, il = lane & 31, h = lane >> 5;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  constexpr int NT = kT2Threads;
+  constexpr int kCQ = kT2S * kT2C / 4 / NT;  // A22 float4 per thread per step (4)
+  constexpr int kLQ = kT2S * kR2 / 4 / NT;   // L21 float4 per thread per step (8)
+  constexpr int CPR = kT2C / 4;
+  auto ldu = [&](int row, int col) -> float4 { return *reinterpret_cast<const float4*>(Ab + (size_t)row * N + col); };
+
+  // ---- the two permutations' tables
+  const int* pb = pperm + b * kPairInts;
+  const int* qb = perm1 + b * kPermInts;
+  const int ndisp = pb[4 * kPairMax] - kR2, ndisp1 = qb[4 * kPermMax] - kOB;
+  bsrc[tid] = pb[2 * kPairMax + tid];
+  if (tid < ndisp) { tdst[tid] = pb[kR2 + tid]; tsrc[tid] = pb[2 * kPairMax + kR2 + tid]; }
+  if (tid < ndisp1) { tdst1[tid] = qb[kOB + tid]; tsrc1[tid] = qb[2 * kPermMax + kOB + tid]; }
+  for (int w = tid; w < nsteps + 2; w += NT) { dbits[w] = 0u; dbits1[w] = 0u; dpre[w] = 0; dpre1[w] = 0; }
+  __syncthreads();
+  int drank = 0, dd = 0, drank1 = 0, dd1 = 0;
+  if (tid < ndisp) {
+    dd = tdst[tid] - c0;
+    for (int j = 0; j < ndisp; ++j) drank += tdst[j] - c0 < dd;
+    dsrc[drank] = tsrc[tid];
+    atomicOr(&dbits[dd >> 5], 1u << (dd & 31));
+  }
+  if (tid < ndisp1) {
+    dd1 = tdst1[tid] - c0;
+    for (int j = 0; j < ndisp1; ++j) drank1 += tdst1[j] - c0 < dd1;
+    dsrc1[drank1] = tsrc1[tid];
+    atomicOr(&dbits1[dd1 >> 5], 1u << (dd1 & 31));
+  }
+  __syncthreads();
+  if (tid < ndisp && __builtin_popcount(dbits[dd >> 5] & ((1u << (dd & 31)) - 1u)) == 0)
+    dpre[dd >> 5] = (unsigned char)drank;
+  if (tid < ndisp1 && __builtin_popcount(dbits1[dd1 >> 5] & ((1u << (dd1 & 31)) - 1u)) == 0)
+    dpre1[dd1 >> 5] = (unsigned char)drank1;
+  // (published by the prologue's barriers)
+
+  // ---- prologue: U12 = L^-1 A12 over the pair's 256 rows, two-level (wave w: strip columns
+  // [32w, 32w + 32); see lu_trail128_kernel's prologue for the register-operand scheme)
+  floatx16 u[8];
+  const int colc = min(cb + 32 * wave + il, N - 1);  // (columns >= N: clamped, never stored)
+  auto mfma = [](float a, float b_, const floatx16& c) { return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b_, c, 0, 0, 0); };
+  // block-row chain j (0..7) against the staged L rows: Lt row 32 (j % 4) + il, the block-t part of
+  // the k range at Lt column 32 i (i < 4) or the block-(t+1) part at coff + 32 (i - 4)
+  auto solve_row_block = [&](int j, int koff_t, int coff) {
+    floatx16 acc = -u[j];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      if (i >= j) break;
+      const int lc = i < 4 ? koff_t + 32 * i : coff + 32 * (i - 4);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float4 l4 = *reinterpret_cast<const float4*>(Lt + (32 * (j & 3) + il) * kP2K + lc + 8 * q + 4 * h);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc = mfma(get4(l4, r), u[i][4 * q + r], acc);
+      }
+    }
+    const int dc = j < 4 ? koff_t + 32 * j : coff + 32 * (j - 4);
+    const floatx16 zero = {};
+    floatx16 o = zero;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const float4 l4 = *reinterpret_cast<const float4*>(Lt + (32 * (j & 3) + il) * kP2K + dc + 8 * q + 4 * h);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) o = mfma(get4(l4, r), acc[4 * q + r], (q == 0 && r == 0) ? zero : o);
+    }
+    u[j] = -o;
+  };
+  auto load_rows = [&](int j0) {  // A12 of pair row blocks [j0, j0 + 4), gathered, accumulator layout
+#pragma unroll
+    for (int j = j0; j < j0 + 4; ++j)
+#pragma unroll
+      for (int v = 0; v < 16; ++v) u[j][v] = Ab[(size_t)bsrc[32 * j + 8 * (v >> 2) + 4 * h + (v & 3)] * N + colc];
+  };
+  // L rows staged by LDS-DMA (global_load_lds, 16 B per lane, no registers): one wave-instruction per
+  // Lt row -- lanes 0..31 its columns [0, 128), lanes 32..63 its columns [128, 256)
+  auto stage_row = [&](int r, const float* lo_src, const float* hi_src) {
+    const float* src = lane < 32 ? lo_src + 4 * lane : hi_src + 4 * (lane - 32);
+    __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)(Lt + r * kP2K), 16, 0, 0);
+  };
+  {  // phase 1: block t's rows, Lt columns [0, 128) = Linv0 (the high half-rows: a harmless copy)
+    const float* Lb = Linv0 + b * (size_t)kLinvFloats;
+    for (int r = wave; r < kOB; r += 4) stage_row(r, Lb + (size_t)r * kOB, Lb + (size_t)r * kOB);
+  }
+  load_rows(0);
+  vm_wait<0>();
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < 4; ++j) solve_row_block(j, 0, 0);
+  __syncthreads();  // Lt consumed
+  {  // phase 2: block t + 1's rows: Lt columns [0, 128) = L21_t of those rows (gathered through block
+     // t + 1's permutation), [128, 256) = Linv1
+    const float* Lb = Linv1 + b * (size_t)kLinvFloats;
+    for (int r = wave; r < kOB; r += 4) stage_row(r, Ab + (size_t)qb[2 * kPermMax + r] * N + P, Lb + (size_t)r * kOB);
+  }
+  load_rows(4);
+  vm_wait<0>();
+  __syncthreads();
+#pragma unroll
+  for (int j = 4; j < 8; ++j) solve_row_block(j, 0, kOB);
+  __syncthreads();  // Lt consumed: U12^T over it
+  // accumulator v of u[j] <-> U12 row 32j + 8(v/4) + 4h + v%4, strip column 32w + il
+#pragma unroll
+  for (int j = 0; j < 8; ++j)
+#pragma unroll
+    for (int v = 0; v < 16; ++v) Ut[(wave * 32 + il) * kP2K + 32 * j + 8 * (v >> 2) + 4 * h + (v & 3)] = u[j][v];
+  __syncthreads();
+  const int wc = wave * 32;
+  float4 ub[kR2 / 8];  // U12[128h + 4sg + 0..3][wc + il]: this wave's MFMA operand for every step
+#pragma unroll
+  for (int sg = 0; sg < kR2 / 8; ++sg)
+    ub[sg] = *reinterpret_cast<const float4*>(Ut + (wc + il) * kP2K + (kR2 / 2) * h + 4 * sg);
+  __syncthreads();  // Ut consumed: Ls / Cb from here on
+
+  // ---- main loop
+  auto loadC = [&](int step, float4 (&c)[kCQ]) {
+    const unsigned m = __builtin_amdgcn_readfirstlane(dbits[step]);
+    const int pre = __builtin_amdgcn_readfirstlane((int)dpre[step]);
+    int srow[kCQ];
+#pragma unroll
+    for (int q = 0; q < kCQ; ++q) {
+      const int ro = (tid + NT * q) / CPR;
+      srow[q] = dsrc[(pre + __builtin_popcount(m & ((1u << ro) - 1u))) & (kPairMax - 1)];
+    }
+#pragma unroll
+    for (int q = 0; q < kCQ; ++q) {
+      const int e = tid + NT * q, ro = e / CPR, row = c0 + step * kT2S + ro, col = cb + (e % CPR) * 4;
+      const int src = ((m >> ro) & 1u) ? srow[q] : row;
+      c[q] = ldu(min(src, N - 1), min(col, N - 4));
+    }
+  };
+  // L21 row (32 per step) = 64 float4 = one wave-row: lanes 0..31 block t's columns (gathered through
+  // block t + 1's permutation), lanes 32..63 block t + 1's columns (in place)
+  auto loadL = [&](int step, float4 (&l)[kLQ]) {
+    const unsigned m = __builtin_amdgcn_readfirstlane(dbits1[step]);
+    const int pre = __builtin_amdgcn_readfirstlane((int)dpre1[step]);
+    const unsigned lo = lane < 32 ? 1u : 0u;
+    const int col = lo ? P + 4 * lane : P1 + 4 * (lane - 32);
+    int s1[kLQ];
+#pragma unroll
+    for (int q = 0; q < kLQ; ++q) {  // (every lane reads a table entry: no branch around the loads)
+      const int ro = wave + 4 * q;
+      s1[q] = dsrc1[(pre + __builtin_popcount(m & ((1u << ro) - 1u))) & (kPermMax - 1)];
+    }
+#pragma unroll
+    for (int q = 0; q < kLQ; ++q) {
+      const int ro = wave + 4 * q, row = c0 + step * kT2S + ro;
+      const int src = ((m >> ro) & lo) ? s1[q] : row;
+      l[q] = ldu(min(src, N - 1), col);
+    }
+  };
+  auto writeL = [&](float* Ls, const float4 (&l)[kLQ]) {
+#pragma unroll
+    for (int q = 0; q < kLQ; ++q) *reinterpret_cast<float4*>(Ls + (wave + 4 * q) * kP2K + 4 * lane) = l[q];
+  };
+  auto storeOut = [&](int step, const float* Cb, float4 (&c)[kCQ]) {
+    float4 pr[kCQ];
+#pragma unroll
+    for (int q = 0; q < kCQ; ++q) {
+      const int e = tid + NT * q;
+      pr[q] = *reinterpret_cast<const float4*>(Cb + (e / CPR) * kT2CS + (e % CPR) * 4);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int q = 0; q < kCQ; ++q) {
+      const int e = tid + NT * q, row = c0 + step * kT2S + e / CPR, col = cb + (e % CPR) * 4;
+      c[q].x -= pr[q].x; c[q].y -= pr[q].y; c[q].z -= pr[q].z; c[q].w -= pr[q].w;
+      if (row < N && col < N) *reinterpret_cast<float4*>(Ab + (size_t)row * N + col) = c[q];
+    }
+  };
+  auto chain = [&](const float* Ls) -> floatx16 {
+    floatx16 acc = {};
+    const floatx16 zero = {};
+    const float* lrow = Ls + il * kP2K + (kR2 / 2) * h;
+    float4 fa[kR2 / 8];
+    __builtin_amdgcn_sched_barrier(0);
+    fa[0] = *reinterpret_cast<const float4*>(lrow);
+    fa[1] = *reinterpret_cast<const float4*>(lrow + 4);
+#pragma unroll
+    for (int sg = 0; sg < kR2 / 8; ++sg) {
+      if (sg + 2 < kR2 / 8) fa[sg + 2] = *reinterpret_cast<const float4*>(lrow + 4 * (sg + 2));
+#pragma unroll
+      for (int s4 = 0; s4 < 4; ++s4)
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(get4(fa[sg], s4), get4(ub[sg], s4), (sg == 0 && s4 == 0) ? zero : acc,
+                                                   0, 0, 0);
+    }
+    __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+#pragma unroll
+    for (int sg = 0; sg < kR2 / 8 - 2; ++sg) {
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
+    }
+    __builtin_amdgcn_sched_group_barrier(0x008, 8, 0);
+    __builtin_amdgcn_sched_barrier(0);
+    return acc;
+  };
+  auto body = [&](int step, float4 (&cc)[kCQ], float4 (&cn)[kCQ], const float4 (&lw)[kLQ], float4 (&lnext)[kLQ]) {
+    const float* Ls = Ls0 + (step & 1) * (kT2S * kP2K);
+    float* Cb = Cb0 + (step & 1) * (kT2S * kT2CS);
+    loadC(step + 1, cn);     // (past the last step: clamped rows, never used)
+    loadL(step + 2, lnext);
+    const floatx16 acc = chain(Ls);
+#pragma unroll
+    for (int v = 0; v < 16; ++v) Cb[(8 * (v >> 2) + 4 * h + (v & 3)) * kT2CS + wc + il] = acc[v];
+    writeL(Ls0 + ((step + 1) & 1) * (kT2S * kP2K), lw);
+    __syncthreads();
+    storeOut(step, Cb, cc);
+  };
+  {
+    float4 c0r[kCQ], c1r[kCQ], la[kLQ], lb[kLQ];
+    loadC(0, c0r);
+    loadL(0, la);
+    loadL(1, lb);
+    writeL(Ls0, la);
+    __syncthreads();
+    int step = 0;
+    for (; step + 1 < nsteps; step += 2) {
+      body(step, c0r, c1r, lb, la);
+      body(step + 1, c1r, c0r, la, lb);
+    }
+    if (step < nsteps) body(step, c0r, c1r, lb, la);
+  }
+  __syncthreads();  // every gathered load of a pair row has completed: U12 to the pair's rows
+  if (cb + wc + il < N) {
+#pragma unroll
+    for (int sg = 0; sg < kR2 / 8; ++sg) {
+      const int i = (kR2 / 2) * h + 4 * sg;
       float* dst = Ab + (size_t)(P + i) * N + cb + wc + il;
       dst[0] = ub[sg].x;
       dst[(size_t)N] = ub[sg].y;
@@ -1649,8 +1972,10 @@ struct iadmm_lu_ctx {
   hipEvent_t fork = nullptr, join = nullptr, ev0 = nullptr, ev1 = nullptr;
 };
 
-static int lu_factor_blocks(int64_t B, int64_t N, float* A, int* piv, int* info, int* perm, int* sig, float* linv,
-                            hipStream_t s0, bool gather, iadmm_lu_ctx* ctx) {
+static int lu_linv_bufs(int64_t N);
+
+static int lu_factor_blocks(int64_t B, int64_t N, float* A, int* piv, int* info, int* perm, int* sig, int* pperm,
+                            float* linv, hipStream_t s0, bool gather, bool pairs, iadmm_lu_ctx* ctx) {
   hipStream_t s = s0;
   const bool vec = (N % 4 == 0) && aligned16(A);
   IADMM_ALLOW_LDS(lu_trail_kernel<true>, kTrailLds);
@@ -1658,9 +1983,16 @@ static int lu_factor_blocks(int64_t B, int64_t N, float* A, int* piv, int* info,
   IADMM_ALLOW_LDS(lu_trail_kernel<false>, kTrailLds);
   IADMM_ALLOW_LDS(lu_trail128_kernel<true>, kT2Lds);
   IADMM_ALLOW_LDS(lu_trail128_kernel<false>, kT2Lds);
+  IADMM_ALLOW_LDS(lu_trail256_kernel, kP2Lds);
   // defer: the interchanges left of each block wait for one final pass (lu_left_*_kernel); every
   // block keeps its permutation in a slot of its own until then
   const bool defer = gather && N <= kLeftDeferMaxN;
+  // paired blocks (r05, opt-in IADMM_LU_PAIRS, with defer and 16-B rows): block t (even) updates only
+  // block t + 1's columns, then one rank-256 update (lu_trail256_kernel) takes everything right of
+  // block t + 1 for both.  Measured slower than the rank-128 default (82.7 vs 78.4 ms at B = 1024,
+  // N = 2000, profiles/r05_lu_paired_*): the rank-256 kernel runs one workgroup per CU and reaches
+  // the rank-128 kernel's rate, not the MFMA ceiling, and every other block loses its look-ahead.
+  const bool paired = pairs && defer && vec;
   const int nb = (int)((N + kOB - 1) / kOB);
   const int64_t slot = B * (int64_t)kPermInts;
   // look-ahead (with a context): block t's trailing update is two launches -- strip 0 (block t + 1's
@@ -1725,17 +2057,39 @@ static int lu_factor_blocks(int64_t B, int64_t N, float* A, int* piv, int* info,
     rc = lu_swap(B, N, P, c2, 0, defer ? 0 : P, gather ? 0 : c2, gather ? 0 : n_, 0, A, piv, pm, s, false);
     if (rc || c2 >= n_) break;
     // U12 = L11^-1 A12 and the rank-128 update of everything right of the block
-    float* lv = linv + (side ? ((P / kOB) & 1) * B * (int64_t)kLinvFloats : 0);
+    const int t = P / kOB;
+    const int nbuf = lu_linv_bufs(N);
+    float* lv = linv + (side || paired ? (t % nbuf) : 0) * B * (int64_t)kLinvFloats;
     hipLaunchKernelGGL(lu_linv_kernel, dim3((unsigned)B), dim3(kOB + 64), 0, s, (int)N, P, A, lv, piv,
                        perm_in_linv ? pm : nullptr, c2);
     LU_TRY_LAUNCH();
+    // pairs: block t even with columns beyond block t + 1 updates only block t + 1's columns (strip
+    // 0); block t + 1 then updates everything right of it for both blocks at rank 256
+    const bool first = paired && (t % 2 == 0) && P + kR2 < n_;
+    const bool second = paired && (t % 2 == 1);  // (t - 1 was a first: its P + 256 = c2 < N here)
+    const int Pp = second ? P - kOB : P;      // the update's own P (the pair's first row)
     const int ntc = ((int)N - c2 + kT2C - 1) / kT2C;
     const int* gp = gather ? pm : nullptr;
+    if (second) {
+      hipLaunchKernelGGL(lu_pair_perm_kernel, dim3((unsigned)B), dim3(64), 0, s, (int)N, Pp, piv, pperm);
+      LU_TRY_LAUNCH();
+    }
+    const float* lv0 = linv + ((t + nbuf - 1) % nbuf) * B * (int64_t)kLinvFloats;  // block t - 1's (pairs)
     auto trail = [&](hipStream_t st, int tc0, int cnt) {
       const dim3 grid((unsigned)(B * cnt));
-      if (vec) hipLaunchKernelGGL(lu_trail128_kernel<true>, grid, dim3(kT2Threads), kT2Lds, st, (int)N, P, cnt, tc0, A, lv, gp);
+      if (second) hipLaunchKernelGGL(lu_trail256_kernel, grid, dim3(kT2Threads), kP2Lds, st, (int)N, Pp, cnt, tc0, A, lv0, lv, pperm, pm);
+      else if (vec) hipLaunchKernelGGL(lu_trail128_kernel<true>, grid, dim3(kT2Threads), kT2Lds, st, (int)N, P, cnt, tc0, A, lv, gp);
       else hipLaunchKernelGGL(lu_trail128_kernel<false>, grid, dim3(kT2Threads), kT2Lds, st, (int)N, P, cnt, tc0, A, lv, gp);
     };
+    if (first) {  // strip 0 only, in order on s (the previous pair's far strips joined first)
+      if (pending) {
+        LU_TRY(hipStreamWaitEvent(s, side->join, 0));
+        pending = false;
+      }
+      trail(s, 0, 1);
+      LU_TRY_LAUNCH();
+      continue;
+    }
     if (!side) {
       trail(s, 0, ntc);
       LU_TRY_LAUNCH();
@@ -1917,9 +2271,15 @@ static int64_t lu_perm_bytes(int64_t B, int64_t N) {  // (two alternating slots 
 static int64_t lu_sig_bytes(int64_t B, int64_t N) {
   return N <= kLeftDeferMaxN ? al16(B * left_sig_off(N, lu_nb(N) - 1) * (int64_t)sizeof(int)) : 0;
 }
-static int64_t lu_ws_bytes(int64_t B, int64_t N) {  // (two L11^-1 buffers with the look-ahead)
-  return lu_perm_bytes(B, N) + lu_sig_bytes(B, N) +
-         (N <= kLuMaxN ? 2 : 1) * B * (int64_t)kLinvFloats * (int64_t)sizeof(float);
+static int64_t lu_pair_bytes(int64_t B, int64_t N) {  // the pair's composed permutation (paired blocks)
+  return N <= kLeftDeferMaxN ? al16(B * (int64_t)kPairInts * (int64_t)sizeof(int)) : 0;
+}
+static int lu_linv_bufs(int64_t N) {  // four with paired blocks, two with the look-ahead
+  return N <= kLeftDeferMaxN ? 4 : (N <= kLuMaxN ? 2 : 1);
+}
+static int64_t lu_ws_bytes(int64_t B, int64_t N) {
+  return lu_perm_bytes(B, N) + lu_sig_bytes(B, N) + lu_pair_bytes(B, N) +
+         lu_linv_bufs(N) * B * (int64_t)kLinvFloats * (int64_t)sizeof(float);
 }
 
 extern "C" int64_t iadmm_lu_factor_ws_bytes(int64_t B, int64_t N) {
@@ -1963,7 +2323,7 @@ extern "C" int iadmm_lu_factor_ex(int64_t B, int64_t N, float* A, int* piv, int*
                                   iadmm_lu_ctx* ctx, int flags, void* stream) {
   if (B <= 0 || N <= 0 || !A || !piv || !info || !ws) return IADMM_E_ARG;
   if (ws_bytes < lu_ws_bytes(B, N)) return IADMM_E_ARG;
-  if (flags & ~IADMM_LU_FORCE_HBM) return IADMM_E_ARG;
+  if (flags & ~(IADMM_LU_FORCE_HBM | IADMM_LU_PAIRS)) return IADMM_E_ARG;
   if (!aligned16(ws)) return IADMM_E_ALIGN;
   if (N > kLuMaxHbmN || B > 0x7fffffff) return IADMM_E_SIZE;
   const int64_t ntc_max = (N + kTC - 1) / kTC, nrc_max = (N + kTRW - 1) / kTRW;
@@ -1979,9 +2339,12 @@ extern "C" int iadmm_lu_factor_ex(int64_t B, int64_t N, float* A, int* piv, int*
   IADMM_CHECK_LAUNCH();
   int* perm = static_cast<int*>(ws);
   int* sig = reinterpret_cast<int*>(static_cast<char*>(ws) + lu_perm_bytes(B, N));
-  float* linv = reinterpret_cast<float*>(static_cast<char*>(ws) + lu_perm_bytes(B, N) + lu_sig_bytes(B, N));
+  int* pperm = reinterpret_cast<int*>(static_cast<char*>(ws) + lu_perm_bytes(B, N) + lu_sig_bytes(B, N));
+  float* linv = reinterpret_cast<float*>(static_cast<char*>(ws) + lu_perm_bytes(B, N) + lu_sig_bytes(B, N) +
+                                         lu_pair_bytes(B, N));
   const bool gather = N <= kLuMaxN && !(flags & IADMM_LU_FORCE_HBM);
-  return lu_factor_blocks(B, N, A, piv, info, perm, sig, linv, s, gather, ctx);
+  const bool pairs = (flags & IADMM_LU_PAIRS) != 0;
+  return lu_factor_blocks(B, N, A, piv, info, perm, sig, pperm, linv, s, gather, pairs, ctx);
 }
 
 extern "C" int iadmm_lu_factor(int64_t B, int64_t N, float* A, int* piv, int* info, void* ws, int64_t ws_bytes,

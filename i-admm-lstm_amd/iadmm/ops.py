@@ -276,6 +276,7 @@ def lu_factor_ws(B, N, device):
 
 
 LU_FORCE_HBM = 1  # include/iadmm.h IADMM_LU_FORCE_HBM (tests)
+LU_PAIRS = 2      # include/iadmm.h IADMM_LU_PAIRS (opt-in rank-256 paired-block updates: A/B and tests)
 
 
 class LuContext:
@@ -315,7 +316,8 @@ def lu_factor(K, ws=None, lookahead=True, flags=0):
     """In-place batched LU with partial pivoting: returns (LU (= K), piv int32 [B,N] 1-based (LAPACK), info int32 [B]).
     ``ws``: a :func:`lu_factor_ws` buffer (allocated per call when omitted).  ``lookahead``: factor the
     next block beside each trailing update on this caller's :func:`lu_context` (N <= 2048; the
-    factors are bit for bit the same either way).  ``flags``: 0 or :data:`LU_FORCE_HBM` (tests)."""
+    factors are bit for bit the same either way).  ``flags``: 0, :data:`LU_FORCE_HBM` and/or :data:`LU_PAIRS`
+    (tests / A/B)."""
     if K.dim() != 3 or K.shape[1] != K.shape[2]:
         raise ValueError(f"K must be [B,N,N], got {tuple(K.shape)}")
     B, N = K.shape[0], K.shape[1]

@@ -129,10 +129,13 @@ int iadmm_kkt_rhs(int64_t B, int64_t n, int64_t m, int64_t num_ineq, const float
  * those of iadmm_lu_factor.  Under stream capture (hipGraph) the call ignores the context and runs
  * every launch on `stream` (the cross-stream fork / join crashed the HIP 7.2 runtime at capture end).
  * A context belongs to the device current at its creation (IADMM_E_ARG on another) and serves one
- * factorization at a time in its streams' order: give each concurrent caller (thread / stream) its own.  flags: 0, or IADMM_LU_FORCE_HBM (tests: the forms for N above
- * the LDS-table limits -- the interchange pass instead of the gathered loads -- at any N). */
+ * factorization at a time in its streams' order: give each concurrent caller (thread / stream) its own.
+ * flags: 0, or IADMM_LU_FORCE_HBM (tests: the forms for N above the LDS-table limits -- the
+ * interchange pass instead of the gathered loads -- at any N), and/or IADMM_LU_PAIRS (opt-in, N <= 2048,
+ * N % 4 == 0: two 128-column blocks share one rank-256 update of the columns right of them -- measured
+ * slower than the default rank-128 updates, kept for study; different rounding, same accuracy). */
 typedef struct iadmm_lu_ctx iadmm_lu_ctx;
-enum { IADMM_LU_FORCE_HBM = 1 };
+enum { IADMM_LU_FORCE_HBM = 1, IADMM_LU_PAIRS = 2 };
 int iadmm_lu_ctx_create(iadmm_lu_ctx** ctx);   /* on the current device; *ctx = NULL on failure */
 int iadmm_lu_ctx_destroy(iadmm_lu_ctx* ctx);   /* waits for the context's streams; NULL is a no-op */
 int64_t iadmm_lu_factor_ws_bytes(int64_t B, int64_t N);

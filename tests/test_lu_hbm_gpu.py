@@ -38,7 +38,7 @@ def _factor_solve(K, b, force):
     from iadmm import ops
     flags = ops.LU_FORCE_HBM if force else 0
     LU, piv, info = ops.lu_factor(K.clone(), flags=flags)
-    x = ops.lu_solve(LU, piv, b, flags=flags)
+    x = ops.lu_solve(LU, piv, b, flags=flags & ops.LU_FORCE_HBM)
     torch.cuda.synchronize()
     return LU, piv, info, x
 

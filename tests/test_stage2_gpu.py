@@ -181,3 +181,44 @@ def test_kkt_assemble_bitwise(n, m):
     ref = orc.kkt_matrix(Q, A0, 6e-6, rho.unsqueeze(-1))
     assert torch.equal(K.cpu(), ref)
     assert torch.equal(torch.signbit(K.cpu()), torch.signbit(ref))
+
+
+@pytest.mark.parametrize("N,B", [(2000, 3), (1024, 2), (516, 2)])
+def test_paired_blocks_match_rank128_form(N, B):
+    """Paired blocks (r05, opt-in IADMM_LU_PAIRS, csrc/lu.hip lu_trail256_kernel: one rank-256 update of
+    the columns right of every two 128-column blocks, the pair's interchanges composed into one gather)
+    against the default rank-128-per-block form on the same KKT-like matrices: a different summation
+    order, so not bitwise -- the pivots must agree, the backward errors ||PLU - K|| / ||K|| stay within
+    1.5x of each other, and both solves land within 2x of each other's distance to the fp64 solution.
+    N = 516: an odd block count with a partial last block (the last pair is a single block)."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from iadmm import ops
+    g = torch.Generator().manual_seed(N + 31)
+    n = N // 2
+    Q = torch.diag_embed(torch.rand(B, n, generator=g)) + 6e-6 * torch.eye(n)
+    A0 = torch.randn(B, N - n, n, generator=g)
+    K = torch.zeros(B, N, N)
+    K[:, :n, :n] = Q
+    K[:, :n, n:] = A0.transpose(1, 2)
+    K[:, n:, :n] = A0
+    K[:, n:, n:] = -torch.diag_embed(torch.where(torch.arange(N - n) < (N - n) // 2, 2.0, 0.002)).expand(B, -1, -1)
+    K = K.cuda()
+    b = torch.randn(B, N, generator=g).cuda()
+    res = {}
+    for name, fl in (("paired", ops.LU_PAIRS), ("rank128", 0)):
+        LU, piv, info = ops.lu_factor(K.clone(), flags=fl)
+        x = ops.lu_solve(LU, piv, b)
+        torch.cuda.synchronize()
+        assert int(info.max()) == 0
+        Kd = K.double()
+        P, L, U = torch.lu_unpack(LU.double(), piv)
+        berr = ((P @ (L @ U) - Kd).flatten(1).norm(dim=1) / Kd.flatten(1).norm(dim=1))
+        x64 = torch.linalg.solve(Kd, b.double())
+        ferr = (x.double() - x64).norm(dim=1) / x64.norm(dim=1)
+        res[name] = (piv, berr, ferr)
+    print(f"[paired N={N}] backward error paired {res['paired'][1].tolist()} rank-128 {res['rank128'][1].tolist()}; "
+          f"forward error paired {res['paired'][2].tolist()} rank-128 {res['rank128'][2].tolist()}")
+    assert torch.equal(res["paired"][0], res["rank128"][0])
+    assert bool((res["paired"][1] <= 1.5 * res["rank128"][1]).all())
+    assert bool((res["paired"][2] <= 2 * res["rank128"][2] + 1e-6).all())

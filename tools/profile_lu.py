@@ -13,6 +13,8 @@ import torch  # noqa: E402
 ap = argparse.ArgumentParser()
 ap.add_argument("--batch", type=int, default=1024)
 ap.add_argument("--N", type=int, default=2000)
+ap.add_argument("--flags", type=int, default=0, help="iadmm_lu_factor_ex flags (2 = IADMM_LU_PAIRS)")
+ap.add_argument("--no-lookahead", action="store_true", help="every launch on one stream (clean durations)")
 a = ap.parse_args()
 from iadmm import data, ops  # noqa: E402
 n = a.N // 2
@@ -22,6 +24,6 @@ rho = torch.full((a.batch, mi + me), 0.5, device="cuda")
 rho[:, mi:] = 500.0
 K = ops.kkt_assemble(d["Q"], d["A0"], 6e-6, None, 0, rho_rows=rho)
 del d
-LU, piv, info = ops.lu_factor(K)
+LU, piv, info = ops.lu_factor(K, flags=a.flags, lookahead=not a.no_lookahead)
 torch.cuda.synchronize()
 print(f"factored B={a.batch} N={a.N}: info max {int(info.max())}")
