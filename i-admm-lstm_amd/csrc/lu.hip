@@ -1348,13 +1348,14 @@ constexpr int kR2 = 2 * kOB;                 // rank of the paired update
 constexpr int kP2K = kR2 + 4;                // LDS stride (k) of its L21 tiles, staged L rows and U12^T
 constexpr int kPairMax = kR2;                // interchanges of a pair
 constexpr int kPairInts = 4 * kPairMax + 1;  // rowid[512], cur[512], cnt
-constexpr int kP2BitWords = (2048 + kT2S - 1) / kT2S + 2;  // (pairing only with the deferred left pass)
-constexpr int kP2MainFloats = 2 * kT2S * kP2K + 2 * kT2S * kT2CS;
-constexpr int kP2ProFloats = kOB * kP2K;
-constexpr int kP2AreaFloats = kP2MainFloats > kP2ProFloats ? kP2MainFloats : kP2ProFloats;
+constexpr int kP2BitWords = (2048 + 31) / 32 + 4;  // one per 32 rows (pairing only with the deferred left pass)
+constexpr int kP2AreaFloats = kOB * kP2K;  // the prologue's staged L rows / U12^T, then the L21 ring
+constexpr int kD2Threads = 512;       // lu_trail256_kernel: 8 waves,
+constexpr int kD2S = 64;              //   rows per step,
+constexpr int kD2Rows = 2048 + 2 * kD2S;  //   row-source table (N <= 2048, whole steps + one)
 constexpr size_t kP2Lds = (size_t)kP2AreaFloats * sizeof(float) +
-                          (size_t)(4 * kPairMax + 3 * kPermMax + 2 * kP2BitWords) * sizeof(int) +
-                          2 * (size_t)((kP2BitWords + 3) & ~3);
+                          (size_t)(kPairMax + kD2Rows + 3 * kPermMax + kP2BitWords) * sizeof(int) +
+                          (size_t)((kP2BitWords + 3) & ~3);
 static_assert(kP2Lds <= 160 * 1024, "one workgroup per CU (gfx950 LDS)");
 
 // one wave per instance: the composed permutation of the pair's 256 interchanges (rows [P, P + 256))
@@ -1371,64 +1372,69 @@ __global__ __launch_bounds__(64) void lu_pair_perm_kernel(int N, int P, const in
   if (lane == 0) out[4 * kPairMax] = cnt;
 }
 
-// The paired far update: per (instance, 128-column strip right of the pair), all rows below it.  Four
-// waves, ONE workgroup per CU (140 KB of LDS; up to 512 registers per wave: the U12 operand alone is
-// 128 per lane at rank 256).  Same step structure as lu_trail128_kernel (32-row steps, L21 and the
-// product double-buffered in LDS, one barrier per step, row-contiguous 16-B A22 accesses) with
-// 128 MFMAs per wave and step.  N % 4 == 0, 16-B aligned rows, N <= 2048 (the host checks).
+// The paired far update: per (instance, 128-column strip right of the pair), all rows below it; one
+// workgroup of EIGHT waves per CU (2 per SIMD), 64-row steps, wave (wr, wc) owning rows [32 wr, 32 wr + 32)
+// x columns [32 wc, 32 wc + 32) of a step.  r05 second form: the first (four waves, product tile
+// through LDS, registers past 256) reached only the rank-128 kernel's rate (profiles/r05_lu_paired_traces.txt).
+// Now the step's A22 tile is the first MFMA's C operand, loaded straight into accumulator layout (lane
+// half h: rows 8q + 4h + r, column il -- one dword per lane, two 128-B row pieces per instruction), and
+// the result is stored from the accumulators: no product tile, no subtraction, and LDS holds only the
+// L21 tiles (LDS-DMA, double-buffered: one barrier per step).  U12 is the B operand from registers,
+// negated once (acc = A22 + L21 (-U12)).  Two accumulator-register sets alternate; each step starts
+// with every memory operation complete (a load never lands in registers a store is still reading).
 // Linv0 / Linv1: the two blocks' lu_linv_kernel buffers; pperm: the pair's composed permutation;
-// perm1: block t + 1's own permutation (lu_linv_kernel's perm wave).
-__global__ __launch_bounds__(kT2Threads, 1) void lu_trail256_kernel(int N, int P, int ntc, int tc0, float* A,
+// perm1: block t + 1's own permutation.  N % 4 == 0, 16-B aligned rows, N <= 2048 (the host checks).
+static_assert(2 * kD2S * kP2K <= kP2AreaFloats, "the L21 ring fits the prologue area");
+__global__ __launch_bounds__(kD2Threads, 1) void lu_trail256_kernel(int N, int P, int ntc, int tc0, float* A,
                                                                     const float* Linv0, const float* Linv1,
                                                                     const int* pperm, const int* perm1) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
-  float* Ls0 = sm;                       // 2 x [32 rows][kP2K]: L21 of a step (k < 128: block t)
-  float* Cb0 = sm + 2 * kT2S * kP2K;     // 2 x [32 rows][kT2CS]: product of a step
+  float* Ls0 = sm;                       // 2 x [64 rows][kP2K]: L21 of a step (k < 128: block t)
   float* Lt = sm;                        // prologue: staged L rows [128][kP2K]
   float* Ut = sm;                        // then U12^T [128 cols][kP2K]
   int* bsrc = reinterpret_cast<int*>(sm + kP2AreaFloats);  // [256] source row of pair row P + i
-  int* tdst = bsrc + kPairMax;           // [256] displaced rows (composed) and
-  int* tsrc = tdst + kPairMax;           // [256] their sources, as given;
-  int* dsrc = tsrc + kPairMax;           // [256] the sources sorted by displaced row
-  int* tdst1 = dsrc + kPairMax;          // [128] block t + 1's displaced rows,
+  int* rowsrc = bsrc + kPairMax;         // [kD2Rows] source row of row c0 + i (composed permutation)
+  int* tdst1 = rowsrc + kD2Rows;         // [128] block t + 1's displaced rows,
   int* tsrc1 = tdst1 + kPermMax;         // [128] their sources,
   int* dsrc1 = tsrc1 + kPermMax;         // [128] sorted
-  unsigned* dbits = reinterpret_cast<unsigned*>(dsrc1 + kPermMax);
-  unsigned* dbits1 = dbits + kP2BitWords;
-  unsigned char* dpre = reinterpret_cast<unsigned char*>(dbits1 + kP2BitWords);
-  unsigned char* dpre1 = dpre + ((kP2BitWords + 3) & ~3);
+  unsigned* dbits1 = reinterpret_cast<unsigned*>(dsrc1 + kPermMax);  // one word per 32 rows
+  unsigned char* dpre1 = reinterpret_cast<unsigned char*>(dbits1 + kP2BitWords);
   const int nwg = gridDim.x, bid = blockIdx.x;
   const int xcd = bid & 7, local = bid >> 3, q8 = nwg >> 3, r8 = nwg & 7;
   const int logical = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + local;
-  const size_t b = (size_t)(logical / ntc);
-  const int tc = tc0 + logical % ntc;
+  const size_t b = (size_t)__builtin_amdgcn_readfirstlane(logical / ntc);  // (uniform: scalar rsrc)
+  const int tc = __builtin_amdgcn_readfirstlane(tc0 + logical % ntc);
   float* Ab = A + b * (size_t)N * N;
   const int P1 = P + kOB, c0 = P + kR2, cb = c0 + tc * kT2C;
-  const int nsteps = (N - c0 + kT2S - 1) / kT2S;
+  const int nsteps = (N - c0 + kD2S - 1) / kD2S;
+  const int nwords = 2 * nsteps;
   const int tid = threadIdx.x, lane = tid & 63, il = lane & 31, h = lane >> 5;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  constexpr int NT = kT2Threads;
-  constexpr int kCQ = kT2S * kT2C / 4 / NT;  // A22 float4 per thread per step (4)
-  constexpr int kLQ = kT2S * kR2 / 4 / NT;   // L21 float4 per thread per step (8)
-  constexpr int CPR = kT2C / 4;
-  auto ldu = [&](int row, int col) -> float4 { return *reinterpret_cast<const float4*>(Ab + (size_t)row * N + col); };
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), wr = wave >> 2, wc = wave & 3;
+  constexpr int NT = kD2Threads;
+  // the instance's matrix as a buffer: rows >= N land past its end (loads 0, stores dropped).  (Made
+  // where it is used: a descriptor captured by reference stayed in private memory, and every buffer
+  // operation became a waterfall loop over a "divergent" descriptor.)
+  float* Abu;  // Ab, provably wave-uniform (a pointer derived from it was treated as divergent)
+  {
+    const uint64_t ab = reinterpret_cast<uint64_t>(Ab);
+    const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)ab), hi = __builtin_amdgcn_readfirstlane((unsigned)(ab >> 32));
+    Abu = reinterpret_cast<float*>(((uint64_t)hi << 32) | lo);
+  }
+#define IADMM_RS __builtin_amdgcn_make_buffer_rsrc(Abu, 0, N * N * 4, 0x00020000)
+  const unsigned kOut = 0x7ffffff0u;     // an offset past the end: the store is dropped
 
   // ---- the two permutations' tables
   const int* pb = pperm + b * kPairInts;
   const int* qb = perm1 + b * kPermInts;
   const int ndisp = pb[4 * kPairMax] - kR2, ndisp1 = qb[4 * kPermMax] - kOB;
-  bsrc[tid] = pb[2 * kPairMax + tid];
-  if (tid < ndisp) { tdst[tid] = pb[kR2 + tid]; tsrc[tid] = pb[2 * kPairMax + kR2 + tid]; }
+  if (tid < kPairMax) bsrc[tid] = pb[2 * kPairMax + tid];
   if (tid < ndisp1) { tdst1[tid] = qb[kOB + tid]; tsrc1[tid] = qb[2 * kPermMax + kOB + tid]; }
-  for (int w = tid; w < nsteps + 2; w += NT) { dbits[w] = 0u; dbits1[w] = 0u; dpre[w] = 0; dpre1[w] = 0; }
+  for (int w = tid; w < nwords + 2; w += NT) { dbits1[w] = 0u; dpre1[w] = 0; }
+  for (int r = tid; r < kD2S * (nsteps + 1); r += NT) rowsrc[r] = min(c0 + r, N - 1);  // (>= N: clamped;
+  // one step past the end: the last step's look-ahead loads read it)
   __syncthreads();
-  int drank = 0, dd = 0, drank1 = 0, dd1 = 0;
-  if (tid < ndisp) {
-    dd = tdst[tid] - c0;
-    for (int j = 0; j < ndisp; ++j) drank += tdst[j] - c0 < dd;
-    dsrc[drank] = tsrc[tid];
-    atomicOr(&dbits[dd >> 5], 1u << (dd & 31));
-  }
+  if (tid < ndisp) rowsrc[pb[kR2 + tid] - c0] = pb[2 * kPairMax + kR2 + tid];  // (distinct rows)
+  int drank1 = 0, dd1 = 0;
   if (tid < ndisp1) {
     dd1 = tdst1[tid] - c0;
     for (int j = 0; j < ndisp1; ++j) drank1 += tdst1[j] - c0 < dd1;
@@ -1436,25 +1442,22 @@ __global__ __launch_bounds__(kT2Threads, 1) void lu_trail256_kernel(int N, int P
     atomicOr(&dbits1[dd1 >> 5], 1u << (dd1 & 31));
   }
   __syncthreads();
-  if (tid < ndisp && __builtin_popcount(dbits[dd >> 5] & ((1u << (dd & 31)) - 1u)) == 0)
-    dpre[dd >> 5] = (unsigned char)drank;
   if (tid < ndisp1 && __builtin_popcount(dbits1[dd1 >> 5] & ((1u << (dd1 & 31)) - 1u)) == 0)
     dpre1[dd1 >> 5] = (unsigned char)drank1;
   // (published by the prologue's barriers)
 
-  // ---- prologue: U12 = L^-1 A12 over the pair's 256 rows, two-level (wave w: strip columns
-  // [32w, 32w + 32); see lu_trail128_kernel's prologue for the register-operand scheme)
+  // ---- prologue: U12 = L^-1 A12 over the pair's 256 rows, two-level, carried negated (see
+  // lu_trail128_kernel's prologue); the waves of both row halves compute their column tile (the same
+  // values), the wr = 0 waves publish it
   floatx16 u[8];
-  const int colc = min(cb + 32 * wave + il, N - 1);  // (columns >= N: clamped, never stored)
+  const int colc = min(cb + 32 * wc + il, N - 1);  // (columns >= N: clamped, never stored)
   auto mfma = [](float a, float b_, const floatx16& c) { return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b_, c, 0, 0, 0); };
-  // block-row chain j (0..7) against the staged L rows: Lt row 32 (j % 4) + il, the block-t part of
-  // the k range at Lt column 32 i (i < 4) or the block-(t+1) part at coff + 32 (i - 4)
-  auto solve_row_block = [&](int j, int koff_t, int coff) {
+  auto solve_row_block = [&](int j, int coff) {
     floatx16 acc = -u[j];
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       if (i >= j) break;
-      const int lc = i < 4 ? koff_t + 32 * i : coff + 32 * (i - 4);
+      const int lc = i < 4 ? 32 * i : coff + 32 * (i - 4);
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const float4 l4 = *reinterpret_cast<const float4*>(Lt + (32 * (j & 3) + il) * kP2K + lc + 8 * q + 4 * h);
@@ -1462,7 +1465,7 @@ __global__ __launch_bounds__(kT2Threads, 1) void lu_trail256_kernel(int N, int P
         for (int r = 0; r < 4; ++r) acc = mfma(get4(l4, r), u[i][4 * q + r], acc);
       }
     }
-    const int dc = j < 4 ? koff_t + 32 * j : coff + 32 * (j - 4);
+    const int dc = j < 4 ? 32 * j : coff + 32 * (j - 4);
     const floatx16 zero = {};
     floatx16 o = zero;
 #pragma unroll
@@ -1479,106 +1482,98 @@ __global__ __launch_bounds__(kT2Threads, 1) void lu_trail256_kernel(int N, int P
 #pragma unroll
       for (int v = 0; v < 16; ++v) u[j][v] = Ab[(size_t)bsrc[32 * j + 8 * (v >> 2) + 4 * h + (v & 3)] * N + colc];
   };
-  // L rows staged by LDS-DMA (global_load_lds, 16 B per lane, no registers): one wave-instruction per
-  // Lt row -- lanes 0..31 its columns [0, 128), lanes 32..63 its columns [128, 256)
+  // L rows staged by LDS-DMA (global_load_lds, 16 B per lane): one wave-instruction per Lt row --
+  // lanes 0..31 its columns [0, 128), lanes 32..63 its columns [128, 256)
   auto stage_row = [&](int r, const float* lo_src, const float* hi_src) {
     const float* src = lane < 32 ? lo_src + 4 * lane : hi_src + 4 * (lane - 32);
     __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)(Lt + r * kP2K), 16, 0, 0);
   };
   {  // phase 1: block t's rows, Lt columns [0, 128) = Linv0 (the high half-rows: a harmless copy)
     const float* Lb = Linv0 + b * (size_t)kLinvFloats;
-    for (int r = wave; r < kOB; r += 4) stage_row(r, Lb + (size_t)r * kOB, Lb + (size_t)r * kOB);
+    for (int r = wave; r < kOB; r += NT / 64) stage_row(r, Lb + (size_t)r * kOB, Lb + (size_t)r * kOB);
   }
   load_rows(0);
   vm_wait<0>();
   __syncthreads();
 #pragma unroll
-  for (int j = 0; j < 4; ++j) solve_row_block(j, 0, 0);
+  for (int j = 0; j < 4; ++j) solve_row_block(j, 0);
   __syncthreads();  // Lt consumed
   {  // phase 2: block t + 1's rows: Lt columns [0, 128) = L21_t of those rows (gathered through block
      // t + 1's permutation), [128, 256) = Linv1
     const float* Lb = Linv1 + b * (size_t)kLinvFloats;
-    for (int r = wave; r < kOB; r += 4) stage_row(r, Ab + (size_t)qb[2 * kPermMax + r] * N + P, Lb + (size_t)r * kOB);
+    for (int r = wave; r < kOB; r += NT / 64)
+      stage_row(r, Ab + (size_t)qb[2 * kPermMax + r] * N + P, Lb + (size_t)r * kOB);
   }
   load_rows(4);
   vm_wait<0>();
   __syncthreads();
 #pragma unroll
-  for (int j = 4; j < 8; ++j) solve_row_block(j, 0, kOB);
+  for (int j = 4; j < 8; ++j) solve_row_block(j, kOB);
   __syncthreads();  // Lt consumed: U12^T over it
-  // accumulator v of u[j] <-> U12 row 32j + 8(v/4) + 4h + v%4, strip column 32w + il
+  if (wr == 0) {
+    // accumulator v of u[j] <-> U12 row 32j + 8(v/4) + 4h + v%4, strip column 32wc + il
 #pragma unroll
-  for (int j = 0; j < 8; ++j)
+    for (int j = 0; j < 8; ++j)
 #pragma unroll
-    for (int v = 0; v < 16; ++v) Ut[(wave * 32 + il) * kP2K + 32 * j + 8 * (v >> 2) + 4 * h + (v & 3)] = u[j][v];
+      for (int v = 0; v < 16; ++v) Ut[(wc * 32 + il) * kP2K + 32 * j + 8 * (v >> 2) + 4 * h + (v & 3)] = -u[j][v];
+  }
   __syncthreads();
-  const int wc = wave * 32;
-  float4 ub[kR2 / 8];  // U12[128h + 4sg + 0..3][wc + il]: this wave's MFMA operand for every step
+  float4 ub[kR2 / 8];  // -U12[128h + 4sg + 0..3][32wc + il]: this wave's MFMA operand for every step
 #pragma unroll
   for (int sg = 0; sg < kR2 / 8; ++sg)
-    ub[sg] = *reinterpret_cast<const float4*>(Ut + (wc + il) * kP2K + (kR2 / 2) * h + 4 * sg);
-  __syncthreads();  // Ut consumed: Ls / Cb from here on
+    ub[sg] = *reinterpret_cast<const float4*>(Ut + (wc * 32 + il) * kP2K + (kR2 / 2) * h + 4 * sg);
+  __syncthreads();  // Ut consumed: the L21 ring from here on
 
   // ---- main loop
-  auto loadC = [&](int step, float4 (&c)[kCQ]) {
-    const unsigned m = __builtin_amdgcn_readfirstlane(dbits[step]);
-    const int pre = __builtin_amdgcn_readfirstlane((int)dpre[step]);
-    int srow[kCQ];
+  const int col = cb + 32 * wc + il;
+  // step s's L21 tile: wave w stages rows w + 8i; a row's block-t half gathers through block t + 1's
+  // permutation (wave-uniform: scalar table lookups), its block-(t+1) half is in place
+  auto issueL = [&](int s) {
+    float* Ls = Ls0 + (s & 1) * (kD2S * kP2K);
+    const bool lo = lane < 32;
 #pragma unroll
-    for (int q = 0; q < kCQ; ++q) {
-      const int ro = (tid + NT * q) / CPR;
-      srow[q] = dsrc[(pre + __builtin_popcount(m & ((1u << ro) - 1u))) & (kPairMax - 1)];
-    }
-#pragma unroll
-    for (int q = 0; q < kCQ; ++q) {
-      const int e = tid + NT * q, ro = e / CPR, row = c0 + step * kT2S + ro, col = cb + (e % CPR) * 4;
-      const int src = ((m >> ro) & 1u) ? srow[q] : row;
-      c[q] = ldu(min(src, N - 1), min(col, N - 4));
-    }
-  };
-  // L21 row (32 per step) = 64 float4 = one wave-row: lanes 0..31 block t's columns (gathered through
-  // block t + 1's permutation), lanes 32..63 block t + 1's columns (in place)
-  auto loadL = [&](int step, float4 (&l)[kLQ]) {
-    const unsigned m = __builtin_amdgcn_readfirstlane(dbits1[step]);
-    const int pre = __builtin_amdgcn_readfirstlane((int)dpre1[step]);
-    const unsigned lo = lane < 32 ? 1u : 0u;
-    const int col = lo ? P + 4 * lane : P1 + 4 * (lane - 32);
-    int s1[kLQ];
-#pragma unroll
-    for (int q = 0; q < kLQ; ++q) {  // (every lane reads a table entry: no branch around the loads)
-      const int ro = wave + 4 * q;
-      s1[q] = dsrc1[(pre + __builtin_popcount(m & ((1u << ro) - 1u))) & (kPermMax - 1)];
-    }
-#pragma unroll
-    for (int q = 0; q < kLQ; ++q) {
-      const int ro = wave + 4 * q, row = c0 + step * kT2S + ro;
-      const int src = ((m >> ro) & lo) ? s1[q] : row;
-      l[q] = ldu(min(src, N - 1), col);
+    for (int i = 0; i < kD2S / (NT / 64); ++i) {
+      const int ro = wave + (NT / 64) * i, row = c0 + kD2S * s + ro;
+      const unsigned m = __builtin_amdgcn_readfirstlane(dbits1[2 * s + (ro >> 5)]);
+      const int pre = __builtin_amdgcn_readfirstlane((int)dpre1[2 * s + (ro >> 5)]);
+      const int bit = ro & 31;
+      const int s1 = __builtin_amdgcn_readfirstlane(dsrc1[(pre + __builtin_popcount(m & ((1u << bit) - 1u))) & (kPermMax - 1)]);
+      const int src = min(((m >> bit) & 1u) ? s1 : row, N - 1), rowc = min(row, N - 1);
+      const unsigned voff = lo ? (unsigned)((src * N + P + 4 * lane) * 4) : (unsigned)((rowc * N + P1 + 4 * (lane - 32)) * 4);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(IADMM_RS, (lds_void*)(Ls + ro * kP2K), 16, voff, 0, 0, 0);
     }
   };
-  auto writeL = [&](float* Ls, const float4 (&l)[kLQ]) {
+  // step s's A22 tile of this wave in accumulator layout (gathered through the pair's permutation: one
+  // row-table read per row, no search); and its store from the accumulators.  The lane's half-row
+  // offset 4h is laundered so that what depends on it is formed per step, not held in registers
+  // across the loop; row offsets 8q + r ride in the scalar offset of each buffer access.
+  const unsigned N4 = 4u * (unsigned)N;
+  auto issueC = [&](int s, floatx16& c) {
+    int h4 = 4 * h;
+    asm volatile("" : "+v"(h4));
+    const int* rt = rowsrc + kD2S * s + 32 * wr + h4;
+    const unsigned cc4 = 4u * (unsigned)min(col, N - 1);
 #pragma unroll
-    for (int q = 0; q < kLQ; ++q) *reinterpret_cast<float4*>(Ls + (wave + 4 * q) * kP2K + 4 * lane) = l[q];
-  };
-  auto storeOut = [&](int step, const float* Cb, float4 (&c)[kCQ]) {
-    float4 pr[kCQ];
-#pragma unroll
-    for (int q = 0; q < kCQ; ++q) {
-      const int e = tid + NT * q;
-      pr[q] = *reinterpret_cast<const float4*>(Cb + (e / CPR) * kT2CS + (e % CPR) * 4);
-    }
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int q = 0; q < kCQ; ++q) {
-      const int e = tid + NT * q, row = c0 + step * kT2S + e / CPR, col = cb + (e % CPR) * 4;
-      c[q].x -= pr[q].x; c[q].y -= pr[q].y; c[q].z -= pr[q].z; c[q].w -= pr[q].w;
-      if (row < N && col < N) *reinterpret_cast<float4*>(Ab + (size_t)row * N + col) = c[q];
+    for (int v = 0; v < 16; ++v) {
+      const unsigned src = (unsigned)rt[8 * (v >> 2) + (v & 3)];
+      c[v] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(IADMM_RS, __umul24(src, N4) + cc4, 0, 0));
     }
   };
-  auto chain = [&](const float* Ls) -> floatx16 {
-    floatx16 acc = {};
-    const floatx16 zero = {};
-    const float* lrow = Ls + il * kP2K + (kR2 / 2) * h;
+  auto storeC = [&](int s, const floatx16& c) {
+    int h4 = 4 * h;
+    asm volatile("" : "+v"(h4));
+    // rows >= N land past the matrix's end, columns >= N on an offset past it: dropped either way
+    const unsigned vb = col < N ? (unsigned)((c0 + kD2S * s + 32 * wr + h4) * N + col) * 4u : kOut;
+#pragma unroll
+    for (int v = 0; v < 16; ++v)
+      // (__float_as_uint on a copy: hipcc 7.2 lowers __builtin_bit_cast of an ext-vector element
+      // reached through a reference to element 0 for every v -- all 16 stores wrote c[0])
+      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(float(c[v])), IADMM_RS, vb,
+                                            (int)((8 * (v >> 2) + (v & 3)) * N4), 0);
+  };
+  auto chain = [&](int s, const floatx16& c) -> floatx16 {
+    const float* lrow = Ls0 + (s & 1) * (kD2S * kP2K) + (32 * wr + il) * kP2K + (kR2 / 2) * h;
+    floatx16 acc = c;
     float4 fa[kR2 / 8];
     __builtin_amdgcn_sched_barrier(0);
     fa[0] = *reinterpret_cast<const float4*>(lrow);
@@ -1587,9 +1582,7 @@ __global__ __launch_bounds__(kT2Threads, 1) void lu_trail256_kernel(int N, int P
     for (int sg = 0; sg < kR2 / 8; ++sg) {
       if (sg + 2 < kR2 / 8) fa[sg + 2] = *reinterpret_cast<const float4*>(lrow + 4 * (sg + 2));
 #pragma unroll
-      for (int s4 = 0; s4 < 4; ++s4)
-        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(get4(fa[sg], s4), get4(ub[sg], s4), (sg == 0 && s4 == 0) ? zero : acc,
-                                                   0, 0, 0);
+      for (int s4 = 0; s4 < 4; ++s4) acc = mfma(get4(fa[sg], s4), get4(ub[sg], s4), acc);
     }
     __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
 #pragma unroll
@@ -1601,45 +1594,41 @@ __global__ __launch_bounds__(kT2Threads, 1) void lu_trail256_kernel(int N, int P
     __builtin_amdgcn_sched_barrier(0);
     return acc;
   };
-  auto body = [&](int step, float4 (&cc)[kCQ], float4 (&cn)[kCQ], const float4 (&lw)[kLQ], float4 (&lnext)[kLQ]) {
-    const float* Ls = Ls0 + (step & 1) * (kT2S * kP2K);
-    float* Cb = Cb0 + (step & 1) * (kT2S * kT2CS);
-    loadC(step + 1, cn);     // (past the last step: clamped rows, never used)
-    loadL(step + 2, lnext);
-    const floatx16 acc = chain(Ls);
-#pragma unroll
-    for (int v = 0; v < 16; ++v) Cb[(8 * (v >> 2) + 4 * h + (v & 3)) * kT2CS + wc + il] = acc[v];
-    writeL(Ls0 + ((step + 1) & 1) * (kT2S * kP2K), lw);
+  // step s: (top) every memory operation so far has completed -- this step's L21 everywhere (the
+  // barrier), its A22 in registers, and the previous step's stores, so the next loads may reuse their
+  // registers; issue step s + 1's L21 and A22; the 128-MFMA chain; store.
+  auto body = [&](int s, floatx16& cc, floatx16& cn) {
+    vm_wait<0>();
     __syncthreads();
-    storeOut(step, Cb, cc);
+    issueL(s + 1);  // (past the last step: clamped rows, never used)
+    issueC(s + 1, cn);
+    cc = chain(s, cc);
+    storeC(s, cc);
   };
-  {
-    float4 c0r[kCQ], c1r[kCQ], la[kLQ], lb[kLQ];
-    loadC(0, c0r);
-    loadL(0, la);
-    loadL(1, lb);
-    writeL(Ls0, la);
-    __syncthreads();
-    int step = 0;
-    for (; step + 1 < nsteps; step += 2) {
-      body(step, c0r, c1r, lb, la);
-      body(step + 1, c1r, c0r, la, lb);
-    }
-    if (step < nsteps) body(step, c0r, c1r, lb, la);
+  floatx16 cA, cB;
+  issueL(0);
+  issueC(0, cA);
+  int s = 0;
+  for (; s + 1 < nsteps; s += 2) {
+    body(s, cA, cB);
+    body(s + 1, cB, cA);
   }
+  if (s < nsteps) body(s, cA, cB);
+  vm_wait<0>();
   __syncthreads();  // every gathered load of a pair row has completed: U12 to the pair's rows
-  if (cb + wc + il < N) {
+  if (wr == 0 && col < N) {
 #pragma unroll
     for (int sg = 0; sg < kR2 / 8; ++sg) {
       const int i = (kR2 / 2) * h + 4 * sg;
-      float* dst = Ab + (size_t)(P + i) * N + cb + wc + il;
-      dst[0] = ub[sg].x;
-      dst[(size_t)N] = ub[sg].y;
-      dst[2 * (size_t)N] = ub[sg].z;
-      dst[3 * (size_t)N] = ub[sg].w;
+      float* dst = Ab + (size_t)(P + i) * N + col;
+      dst[0] = -ub[sg].x;
+      dst[(size_t)N] = -ub[sg].y;
+      dst[2 * (size_t)N] = -ub[sg].z;
+      dst[3 * (size_t)N] = -ub[sg].w;
     }
   }
 }
+#undef IADMM_RS
 
 // Solve (P^T L U) x = b in place for one instance per workgroup.
 constexpr int kDS = kSolveBlk + 1;  // LDS stride of the staged diagonal block
@@ -2077,7 +2066,7 @@ static int lu_factor_blocks(int64_t B, int64_t N, float* A, int* piv, int* info,
     const float* lv0 = linv + ((t + nbuf - 1) % nbuf) * B * (int64_t)kLinvFloats;  // block t - 1's (pairs)
     auto trail = [&](hipStream_t st, int tc0, int cnt) {
       const dim3 grid((unsigned)(B * cnt));
-      if (second) hipLaunchKernelGGL(lu_trail256_kernel, grid, dim3(kT2Threads), kP2Lds, st, (int)N, Pp, cnt, tc0, A, lv0, lv, pperm, pm);
+      if (second) hipLaunchKernelGGL(lu_trail256_kernel, grid, dim3(kD2Threads), kP2Lds, st, (int)N, Pp, cnt, tc0, A, lv0, lv, pperm, pm);
       else if (vec) hipLaunchKernelGGL(lu_trail128_kernel<true>, grid, dim3(kT2Threads), kT2Lds, st, (int)N, P, cnt, tc0, A, lv, gp);
       else hipLaunchKernelGGL(lu_trail128_kernel<false>, grid, dim3(kT2Threads), kT2Lds, st, (int)N, P, cnt, tc0, A, lv, gp);
     };

@@ -188,7 +188,7 @@ def test_paired_blocks_match_rank128_form(N, B):
     """Paired blocks (r05, opt-in IADMM_LU_PAIRS, csrc/lu.hip lu_trail256_kernel: one rank-256 update of
     the columns right of every two 128-column blocks, the pair's interchanges composed into one gather)
     against the default rank-128-per-block form on the same KKT-like matrices: a different summation
-    order, so not bitwise -- the pivots must agree, the backward errors ||PLU - K|| / ||K|| stay within
+    order, so not bitwise -- the backward errors ||PLU - K|| / ||K|| stay within
     1.5x of each other, and both solves land within 2x of each other's distance to the fp64 solution.
     N = 516: an odd block count with a partial last block (the last pair is a single block)."""
     if not torch.cuda.is_available():
@@ -219,6 +219,8 @@ def test_paired_blocks_match_rank128_form(N, B):
         res[name] = (piv, berr, ferr)
     print(f"[paired N={N}] backward error paired {res['paired'][1].tolist()} rank-128 {res['rank128'][1].tolist()}; "
           f"forward error paired {res['paired'][2].tolist()} rank-128 {res['rank128'][2].tolist()}")
-    assert torch.equal(res["paired"][0], res["rank128"][0])
+    # (no pivot comparison: a different summation order breaks near-ties in the pivot search, and one
+    # different pivot changes every later one -- measured 88 % agreement at N = 2000 with equal
+    # backward errors; the factorisation is pinned by its backward error instead)
     assert bool((res["paired"][1] <= 1.5 * res["rank128"][1]).all())
     assert bool((res["paired"][2] <= 2 * res["rank128"][2] + 1e-6).all())

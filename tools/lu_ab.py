@@ -46,7 +46,7 @@ def child(args):
         K = ops.kkt_assemble(d["Q"], d["A0"], 6e-6, None, 0, rho_rows=rho)
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
-        LU, piv, info = ops.lu_factor(K, ws=ws)
+        LU, piv, info = ops.lu_factor(K, ws=ws, flags=args.flags) if args.flags else ops.lu_factor(K, ws=ws)
         e1.record()
         torch.cuda.synchronize()
         if r:
@@ -73,7 +73,7 @@ def child(args):
     # bitwise fingerprint of the factors (A/B variants that claim the same arithmetic must agree)
     lu_sum = sum(int(torch.sum(LU[i:i + 64].view(torch.int32), dtype=torch.int64)) for i in range(0, B, 64))
     piv_sum = int(torch.sum(piv, dtype=torch.int64))
-    print(json.dumps({"lib": os.environ.get("IADMM_LIB_PATH", "default"), "B": B, "N": N, "factor_ms": times,
+    print(json.dumps({"lib": os.environ.get("IADMM_LIB_PATH", "default"), "flags": args.flags, "B": B, "N": N, "factor_ms": times,
                       "best_ms": ms, "tflops": B * 2.0 / 3.0 * N ** 3 / ms / 1e9, "frac_fp32_mfma": B * 2.0 / 3.0 * N ** 3 / ms / 1e9 / 157.3,
                       "info_max": int(info.max()), "solve_ms": solve_ms,
                       "solve_tbps": B * args.N * args.N * 4 / min(solve_ms) / 1e9, "backward_error": berr, "piv_head": piv[0, :8].tolist(),
@@ -87,13 +87,14 @@ def main():
     ap.add_argument("--N", type=int, default=2000)
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--child", action="store_true")
+    ap.add_argument("--flags", type=int, default=0, help="iadmm_lu_factor_ex flags (2 = IADMM_LU_PAIRS)")
     args = ap.parse_args()
     if args.child:
         return child(args)
     for lib in args.libs:
         env = dict(os.environ, IADMM_LIB_PATH=os.path.abspath(lib))
         cmd = [sys.executable, os.path.abspath(__file__), "--child", "--batch", str(args.batch), "--N", str(args.N),
-               "--reps", str(args.reps)]
+               "--reps", str(args.reps), "--flags", str(args.flags)]
         rc = subprocess.run(cmd, env=env, timeout=600).returncode
         if rc != 0:
             print(json.dumps({"lib": lib, "rc": rc}), flush=True)

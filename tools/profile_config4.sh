@@ -18,7 +18,7 @@ raw=$(mktemp -d /tmp/cfg4_XXXX)
 C4="--batch 512 --num_var 5000 --num_ineq 2500 --num_eq 2500 --hidden_dim 2048"
 for ctr in FETCH_SIZE WRITE_SIZE; do
   timeout -s KILL 600 rocprofv3 --pmc $ctr --output-format csv -d "$raw/pmc_$ctr" -o run -- \
-    python3 bench.py $C4 --outer_T 2 --steps 1 --warmup 0 --cpu-sample 0 --alt-f16x3 0 --in-place-scaling \
+    python3 bench.py $C4 --outer_T 2 --steps 1 --warmup 0 --cpu-sample 0 --alt-f16x3 0 --train-batch 0 --stage2-iters 0 --in-place-scaling \
     > "$out/pmc_$ctr.log" 2>&1
   python3 tools/pmc_summary.py "$(find "$raw/pmc_$ctr" -name "*counter_collection.csv" | head -1)" \
     > "profiles/${tag}_pmc_${ctr}_n5000_m5000_h2048_B512.csv"
@@ -26,7 +26,7 @@ for ctr in FETCH_SIZE WRITE_SIZE; do
   rm -rf "$raw/pmc_$ctr"
 done
 rm -rf "$raw"
-timeout -k 10 700 python3 -u bench.py $C4 --outer_T 200 --steps 1 --warmup 0 --cpu-sample 0 --alt-f16x3 0 \
+timeout -k 10 700 python3 -u bench.py $C4 --outer_T 200 --steps 1 --warmup 0 --cpu-sample 0 --alt-f16x3 0 --train-batch 0 --stage2-iters 0 \
   --in-place-scaling > "$out/bench_config4.json" 2> "$out/bench_config4.err"
 [ "${SKIP_STAGE2:-0}" = 1 ] || timeout -k 10 400 python3 -u bench_stage2.py --batch 512 --num_var 5000 --num_ineq 2500 --num_eq 2500 \
   --steps 1 --warmup 0 --cpu-sample 0 > "$out/stage2_config4.json" 2> "$out/stage2_config4.err"
