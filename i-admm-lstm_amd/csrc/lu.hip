@@ -1345,18 +1345,18 @@ __global__ __launch_bounds__(kT2Threads, 2) void lu_trail128_kernel(int N, int P
 // permutation.  A displaced row's source is always one of the pair's 256 block rows, which take U12
 // only after the last step's loads (as in lu_trail128_kernel).
 constexpr int kR2 = 2 * kOB;                 // rank of the paired update
-constexpr int kP2K = kR2 + 4;                // LDS stride (k) of its L21 tiles, staged L rows and U12^T
+constexpr int kP2K = kR2 + 4;                // LDS stride (k) of its L21 tiles and staged L rows
 constexpr int kPairMax = kR2;                // interchanges of a pair
 constexpr int kPairInts = 4 * kPairMax + 1;  // rowid[512], cur[512], cnt
-constexpr int kP2BitWords = (2048 + 31) / 32 + 4;  // one per 32 rows (pairing only with the deferred left pass)
-constexpr int kP2AreaFloats = kOB * kP2K;  // the prologue's staged L rows / U12^T, then the L21 ring
-constexpr int kD2Threads = 512;       // lu_trail256_kernel: 8 waves,
-constexpr int kD2S = 64;              //   rows per step,
-constexpr int kD2Rows = 2048 + 2 * kD2S;  //   row-source table (N <= 2048, whole steps + one)
+constexpr int kD2Threads = 256;              // lu_trail256_kernel: 4 waves, two workgroups per CU,
+constexpr int kD2S = 32;                     //   rows per step,
+constexpr int kD2Rows = 2048 + 2 * kD2S;     //   row-source table (N <= 2048, whole steps + one)
+constexpr int kP2BitWords = (2048 + 31) / 32 + 4;  // one per step (pairing only with the deferred left pass)
+constexpr int kP2AreaFloats = 2 * kD2S * kP2K;     // the L21 ring (two steps) = the prologue's 64 staged L rows
 constexpr size_t kP2Lds = (size_t)kP2AreaFloats * sizeof(float) +
                           (size_t)(kPairMax + kD2Rows + 3 * kPermMax + kP2BitWords) * sizeof(int) +
                           (size_t)((kP2BitWords + 3) & ~3);
-static_assert(kP2Lds <= 160 * 1024, "one workgroup per CU (gfx950 LDS)");
+static_assert(2 * kP2Lds <= 160 * 1024, "two workgroups per CU (gfx950 LDS)");
 
 // one wave per instance: the composed permutation of the pair's 256 interchanges (rows [P, P + 256))
 __global__ __launch_bounds__(64) void lu_pair_perm_kernel(int N, int P, const int* piv, int* pperm) {
@@ -1372,33 +1372,50 @@ __global__ __launch_bounds__(64) void lu_pair_perm_kernel(int N, int P, const in
   if (lane == 0) out[4 * kPairMax] = cnt;
 }
 
-// The paired far update: per (instance, 128-column strip right of the pair), all rows below it; one
-// workgroup of EIGHT waves per CU (2 per SIMD), 64-row steps, wave (wr, wc) owning rows [32 wr, 32 wr + 32)
-// x columns [32 wc, 32 wc + 32) of a step.  r05 second form: the first (four waves, product tile
-// through LDS, registers past 256) reached only the rank-128 kernel's rate (profiles/r05_lu_paired_traces.txt).
-// Now the step's A22 tile is the first MFMA's C operand, loaded straight into accumulator layout (lane
-// half h: rows 8q + 4h + r, column il -- one dword per lane, two 128-B row pieces per instruction), and
-// the result is stored from the accumulators: no product tile, no subtraction, and LDS holds only the
-// L21 tiles (LDS-DMA, double-buffered: one barrier per step).  U12 is the B operand from registers,
-// negated once (acc = A22 + L21 (-U12)).  Two accumulator-register sets alternate; each step starts
-// with every memory operation complete (a load never lands in registers a store is still reading).
-// Linv0 / Linv1: the two blocks' lu_linv_kernel buffers; pperm: the pair's composed permutation;
-// perm1: block t + 1's own permutation.  N % 4 == 0, 16-B aligned rows, N <= 2048 (the host checks).
-static_assert(2 * kD2S * kP2K <= kP2AreaFloats, "the L21 ring fits the prologue area");
-__global__ __launch_bounds__(kD2Threads, 1) void lu_trail256_kernel(int N, int P, int ntc, int tc0, float* A,
+// The paired far update: per (instance, 128-column strip right of the pair), all rows below it.  r05
+// third form: TWO workgroups of four waves per CU (2 waves per SIMD), 32-row steps, wave w owning the
+// strip's columns [32w, 32w + 32).  (The first form, four waves with the product tile through LDS, and
+// the second, one 8-wave workgroup per CU with 64-row steps, ran at ~0.6 of MFMA: their prologue was
+// computed twice (both row halves) and a step's memory work and barrier stalled the whole CU --
+// profiles/r05_lubench256.txt.)
+//   prologue: U12 = L^-1 A12 over the pair's 256 rows, two-level, carried negated (see
+//             lu_trail128_kernel's prologue), 64 staged L rows (two 32-row blocks) at a time; wave w
+//             computes only its own 32 columns.  U12 stays in registers in accumulator layout (block
+//             j, register v: row 32j + 8(v/4) + 4h + v%4, column il) and is the main loop's B operand
+//             as it is: the k index of an MFMA pair is (32j + 8q + r, 32j + 8q + 4 + r), lane half h
+//             taking the second, so the matching L21 entries (four consecutive k) are one 16-B LDS read;
+//   main loop: the step's A22 tile is the first MFMA's C operand, loaded straight into accumulator
+//             layout (one dword per lane, two 128-B row pieces per instruction), and the result is
+//             stored from the accumulators (buffer stores; rows / columns >= N dropped by the range
+//             check).  L21 comes by LDS-DMA into a two-step ring (one barrier per step).  The memory
+//             work of step s + 1 (A22 loads, L21 DMA) and the stores of step s - 1 ride inside step s's
+//             128-MFMA chain; three accumulator-register sets rotate (A22 (s) / result (s - 1) being
+//             stored / A22 (s + 1) being loaded): the compiler holds a store's data registers until
+//             the store completes (gfx9: one vmcnt for loads and stores).  The L21 fragments are read
+//             by inline-asm ds_read_b128 with explicit lgkmcnt waits: the compiler treats every LDS
+//             read as possibly aliasing an in-flight LDS-DMA and would drain vmcnt before it (the ring
+//             slot read is never the one the DMA fills).
+// Interchanges: A22 and A12 rows gather through the pair's composed permutation (pperm: a row-source
+// table, no search); L21's block-t half gathers through block t + 1's own permutation (perm1).  A
+// displaced row's source is one of the pair's 256 rows, which take U12 only after the last step's loads.
+// Linv0 / Linv1: the two blocks' lu_linv_kernel buffers.  N % 4 == 0, 16-B aligned rows, N <= 2048
+// (the host checks).  MODE: tools/lubench256.hip's timing diagnostics only (results meaningless):
+// 4 = no main-loop memory work, 8 = one VALU op per main-loop MFMA instead, 16 = no prologue MFMAs.
+template <int MODE = 0>
+__global__ __launch_bounds__(kD2Threads, 2) void lu_trail256_kernel(int N, int P, int ntc, int tc0, float* A,
                                                                     const float* Linv0, const float* Linv1,
                                                                     const int* pperm, const int* perm1) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
-  float* Ls0 = sm;                       // 2 x [64 rows][kP2K]: L21 of a step (k < 128: block t)
-  float* Lt = sm;                        // prologue: staged L rows [128][kP2K]
-  float* Ut = sm;                        // then U12^T [128 cols][kP2K]
+  float* Ls0 = sm;                       // 2 x [32 rows][kP2K]: L21 of a step
+  float* Lt = sm;                        // prologue: 64 staged L rows [64][kP2K]
   int* bsrc = reinterpret_cast<int*>(sm + kP2AreaFloats);  // [256] source row of pair row P + i
   int* rowsrc = bsrc + kPairMax;         // [kD2Rows] source row of row c0 + i (composed permutation)
   int* tdst1 = rowsrc + kD2Rows;         // [128] block t + 1's displaced rows,
   int* tsrc1 = tdst1 + kPermMax;         // [128] their sources,
   int* dsrc1 = tsrc1 + kPermMax;         // [128] sorted
-  unsigned* dbits1 = reinterpret_cast<unsigned*>(dsrc1 + kPermMax);  // one word per 32 rows
+  unsigned* dbits1 = reinterpret_cast<unsigned*>(dsrc1 + kPermMax);  // one word per step
   unsigned char* dpre1 = reinterpret_cast<unsigned char*>(dbits1 + kP2BitWords);
+  constexpr bool kNoMem = (MODE & 4) != 0, kNoMfma = (MODE & 8) != 0, kNoPro = (MODE & 16) != 0;
   const int nwg = gridDim.x, bid = blockIdx.x;
   const int xcd = bid & 7, local = bid >> 3, q8 = nwg >> 3, r8 = nwg & 7;
   const int logical = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + local;
@@ -1407,10 +1424,9 @@ __global__ __launch_bounds__(kD2Threads, 1) void lu_trail256_kernel(int N, int P
   float* Ab = A + b * (size_t)N * N;
   const int P1 = P + kOB, c0 = P + kR2, cb = c0 + tc * kT2C;
   const int nsteps = (N - c0 + kD2S - 1) / kD2S;
-  const int nwords = 2 * nsteps;
   const int tid = threadIdx.x, lane = tid & 63, il = lane & 31, h = lane >> 5;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), wr = wave >> 2, wc = wave & 3;
-  constexpr int NT = kD2Threads;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  constexpr int NT = kD2Threads, NW = NT / 64;
   // the instance's matrix as a buffer: rows >= N land past its end (loads 0, stores dropped).  (Made
   // where it is used: a descriptor captured by reference stayed in private memory, and every buffer
   // operation became a waterfall loop over a "divergent" descriptor.)
@@ -1427,13 +1443,13 @@ __global__ __launch_bounds__(kD2Threads, 1) void lu_trail256_kernel(int N, int P
   const int* pb = pperm + b * kPairInts;
   const int* qb = perm1 + b * kPermInts;
   const int ndisp = pb[4 * kPairMax] - kR2, ndisp1 = qb[4 * kPermMax] - kOB;
-  if (tid < kPairMax) bsrc[tid] = pb[2 * kPairMax + tid];
+  for (int i = tid; i < kPairMax; i += NT) bsrc[i] = pb[2 * kPairMax + i];
   if (tid < ndisp1) { tdst1[tid] = qb[kOB + tid]; tsrc1[tid] = qb[2 * kPermMax + kOB + tid]; }
-  for (int w = tid; w < nwords + 2; w += NT) { dbits1[w] = 0u; dpre1[w] = 0; }
+  for (int w = tid; w < nsteps + 2; w += NT) { dbits1[w] = 0u; dpre1[w] = 0; }
   for (int r = tid; r < kD2S * (nsteps + 1); r += NT) rowsrc[r] = min(c0 + r, N - 1);  // (>= N: clamped;
   // one step past the end: the last step's look-ahead loads read it)
   __syncthreads();
-  if (tid < ndisp) rowsrc[pb[kR2 + tid] - c0] = pb[2 * kPairMax + kR2 + tid];  // (distinct rows)
+  for (int i = tid; i < ndisp; i += NT) rowsrc[pb[kR2 + i] - c0] = pb[2 * kPairMax + kR2 + i];  // (distinct rows)
   int drank1 = 0, dd1 = 0;
   if (tid < ndisp1) {
     dd1 = tdst1[tid] - c0;
@@ -1446,186 +1462,175 @@ __global__ __launch_bounds__(kD2Threads, 1) void lu_trail256_kernel(int N, int P
     dpre1[dd1 >> 5] = (unsigned char)drank1;
   // (published by the prologue's barriers)
 
-  // ---- prologue: U12 = L^-1 A12 over the pair's 256 rows, two-level, carried negated (see
-  // lu_trail128_kernel's prologue); the waves of both row halves compute their column tile (the same
-  // values), the wr = 0 waves publish it
+  // ---- prologue: U_j = Linv_jj (A_j - sum_{i<j} L_ji U_i), j = 0..7, carried negated; this wave's columns
   floatx16 u[8];
-  const int colc = min(cb + 32 * wc + il, N - 1);  // (columns >= N: clamped, never stored)
+  const int col = cb + 32 * wave + il;
+  const int colc = min(col, N - 1);  // (columns >= N: clamped, never stored)
   auto mfma = [](float a, float b_, const floatx16& c) { return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b_, c, 0, 0, 0); };
-  auto solve_row_block = [&](int j, int coff) {
+  auto solve_row_block = [&](int j) {  // staged L rows: block j's are Lt rows 32 (j & 1) + [0, 32)
+    const float* lr = Lt + (32 * (j & 1) + il) * kP2K + 4 * h;
     floatx16 acc = -u[j];
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       if (i >= j) break;
-      const int lc = i < 4 ? 32 * i : coff + 32 * (i - 4);
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        const float4 l4 = *reinterpret_cast<const float4*>(Lt + (32 * (j & 3) + il) * kP2K + lc + 8 * q + 4 * h);
+        const float4 l4 = *reinterpret_cast<const float4*>(lr + 32 * i + 8 * q);
 #pragma unroll
         for (int r = 0; r < 4; ++r) acc = mfma(get4(l4, r), u[i][4 * q + r], acc);
       }
     }
-    const int dc = j < 4 ? 32 * j : coff + 32 * (j - 4);
     const floatx16 zero = {};
     floatx16 o = zero;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      const float4 l4 = *reinterpret_cast<const float4*>(Lt + (32 * (j & 3) + il) * kP2K + dc + 8 * q + 4 * h);
+      const float4 l4 = *reinterpret_cast<const float4*>(lr + 32 * j + 8 * q);
 #pragma unroll
       for (int r = 0; r < 4; ++r) o = mfma(get4(l4, r), acc[4 * q + r], (q == 0 && r == 0) ? zero : o);
     }
     u[j] = -o;
   };
-  auto load_rows = [&](int j0) {  // A12 of pair row blocks [j0, j0 + 4), gathered, accumulator layout
-#pragma unroll
-    for (int j = j0; j < j0 + 4; ++j)
-#pragma unroll
-      for (int v = 0; v < 16; ++v) u[j][v] = Ab[(size_t)bsrc[32 * j + 8 * (v >> 2) + 4 * h + (v & 3)] * N + colc];
-  };
-  // L rows staged by LDS-DMA (global_load_lds, 16 B per lane): one wave-instruction per Lt row --
-  // lanes 0..31 its columns [0, 128), lanes 32..63 its columns [128, 256)
+  // a staged L row (LDS-DMA, 16 B per lane): lanes 0..31 its columns [0, 128), lanes 32..63 [128, 256)
   auto stage_row = [&](int r, const float* lo_src, const float* hi_src) {
     const float* src = lane < 32 ? lo_src + 4 * lane : hi_src + 4 * (lane - 32);
     __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)(Lt + r * kP2K), 16, 0, 0);
   };
-  {  // phase 1: block t's rows, Lt columns [0, 128) = Linv0 (the high half-rows: a harmless copy)
-    const float* Lb = Linv0 + b * (size_t)kLinvFloats;
-    for (int r = wave; r < kOB; r += NT / 64) stage_row(r, Lb + (size_t)r * kOB, Lb + (size_t)r * kOB);
+#pragma unroll
+  for (int ph = 0; ph < 4; ++ph) {
+    // pair rows [64 ph, 64 ph + 64): block t's rows hold Linv0 (columns [0, 128); the high half-row a
+    // harmless copy); block t + 1's rows hold L21_t of those rows (gathered through block t + 1's
+    // permutation) in [0, 128) and Linv1 in [128, 256)
+    for (int r = wave; r < 2 * kD2S; r += NW) {
+      const int pr = 64 * ph + r;
+      if (ph < 2) {
+        const float* Lb = Linv0 + b * (size_t)kLinvFloats + (size_t)pr * kOB;
+        stage_row(r, Lb, Lb);
+      } else {
+        stage_row(r, Ab + (size_t)qb[2 * kPermMax + pr - kOB] * N + P, Linv1 + b * (size_t)kLinvFloats + (size_t)(pr - kOB) * kOB);
+      }
+    }
+#pragma unroll
+    for (int j = 2 * ph; j < 2 * ph + 2; ++j)
+#pragma unroll
+      for (int v = 0; v < 16; ++v) u[j][v] = Ab[(size_t)bsrc[32 * j + 8 * (v >> 2) + 4 * h + (v & 3)] * N + colc];
+    vm_wait<0>();
+    __syncthreads();
+    if (!kNoPro) {
+      solve_row_block(2 * ph);
+      solve_row_block(2 * ph + 1);
+    }
+    __syncthreads();  // Lt consumed
   }
-  load_rows(0);
-  vm_wait<0>();
-  __syncthreads();
 #pragma unroll
-  for (int j = 0; j < 4; ++j) solve_row_block(j, 0);
-  __syncthreads();  // Lt consumed
-  {  // phase 2: block t + 1's rows: Lt columns [0, 128) = L21_t of those rows (gathered through block
-     // t + 1's permutation), [128, 256) = Linv1
-    const float* Lb = Linv1 + b * (size_t)kLinvFloats;
-    for (int r = wave; r < kOB; r += NT / 64)
-      stage_row(r, Ab + (size_t)qb[2 * kPermMax + r] * N + P, Lb + (size_t)r * kOB);
-  }
-  load_rows(4);
-  vm_wait<0>();
-  __syncthreads();
-#pragma unroll
-  for (int j = 4; j < 8; ++j) solve_row_block(j, kOB);
-  __syncthreads();  // Lt consumed: U12^T over it
-  if (wr == 0) {
-    // accumulator v of u[j] <-> U12 row 32j + 8(v/4) + 4h + v%4, strip column 32wc + il
-#pragma unroll
-    for (int j = 0; j < 8; ++j)
-#pragma unroll
-      for (int v = 0; v < 16; ++v) Ut[(wc * 32 + il) * kP2K + 32 * j + 8 * (v >> 2) + 4 * h + (v & 3)] = -u[j][v];
-  }
-  __syncthreads();
-  float4 ub[kR2 / 8];  // -U12[128h + 4sg + 0..3][32wc + il]: this wave's MFMA operand for every step
-#pragma unroll
-  for (int sg = 0; sg < kR2 / 8; ++sg)
-    ub[sg] = *reinterpret_cast<const float4*>(Ut + (wc * 32 + il) * kP2K + (kR2 / 2) * h + 4 * sg);
-  __syncthreads();  // Ut consumed: the L21 ring from here on
+  for (int j = 0; j < 8; ++j) u[j] = -u[j];  // -U12: acc = A22 + L21 (-U12)
 
   // ---- main loop
-  const int col = cb + 32 * wc + il;
-  // step s's L21 tile: wave w stages rows w + 8i; a row's block-t half gathers through block t + 1's
-  // permutation (wave-uniform: scalar table lookups), its block-(t+1) half is in place
-  auto issueL = [&](int s) {
+  const unsigned N4 = 4u * (unsigned)N;
+  // (the lane's half-row offset 4h is laundered so that what depends on it is formed per use, not held
+  // in registers across the loop; row offsets 8q + r ride in the scalar offset of each buffer access)
+  auto storeQ = [&](int s, const floatx16& c, int q) {  // 4 of a step's 16 stores (s < 0: dropped)
+    int h4 = 4 * h;
+    asm volatile("" : "+v"(h4));
+    const unsigned vb = (s >= 0 && col < N) ? (unsigned)((c0 + kD2S * s + h4) * N + col) * 4u : kOut;
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      // (__float_as_uint on a copy: hipcc 7.2 lowers __builtin_bit_cast of an ext-vector element
+      // reached through a reference to element 0 for every v -- all 16 stores wrote c[0])
+      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(float(c[4 * q + r])), IADMM_RS, vb, (int)((8 * q + r) * N4), 0);
+  };
+  // 2 of this wave's 8 L21 rows of step s (rows wave + 4i): the block-t half gathers through block t + 1's
+  // permutation (wave-uniform: scalar table lookups), the block-(t+1) half is in place
+  auto issueLQ = [&](int s, int q) {
     float* Ls = Ls0 + (s & 1) * (kD2S * kP2K);
     const bool lo = lane < 32;
+    const unsigned m = __builtin_amdgcn_readfirstlane(dbits1[s]);
+    const int pre = __builtin_amdgcn_readfirstlane((int)dpre1[s]);
 #pragma unroll
-    for (int i = 0; i < kD2S / (NT / 64); ++i) {
-      const int ro = wave + (NT / 64) * i, row = c0 + kD2S * s + ro;
-      const unsigned m = __builtin_amdgcn_readfirstlane(dbits1[2 * s + (ro >> 5)]);
-      const int pre = __builtin_amdgcn_readfirstlane((int)dpre1[2 * s + (ro >> 5)]);
-      const int bit = ro & 31;
-      const int s1 = __builtin_amdgcn_readfirstlane(dsrc1[(pre + __builtin_popcount(m & ((1u << bit) - 1u))) & (kPermMax - 1)]);
-      const int src = min(((m >> bit) & 1u) ? s1 : row, N - 1), rowc = min(row, N - 1);
+    for (int i = 2 * q; i < 2 * q + 2; ++i) {
+      const int ro = wave + NW * i, row = c0 + kD2S * s + ro;
+      const int s1 = __builtin_amdgcn_readfirstlane(dsrc1[(pre + __builtin_popcount(m & ((1u << ro) - 1u))) & (kPermMax - 1)]);
+      const int src = min(((m >> ro) & 1u) ? s1 : row, N - 1), rowc = min(row, N - 1);
       const unsigned voff = lo ? (unsigned)((src * N + P + 4 * lane) * 4) : (unsigned)((rowc * N + P1 + 4 * (lane - 32)) * 4);
       __builtin_amdgcn_raw_ptr_buffer_load_lds(IADMM_RS, (lds_void*)(Ls + ro * kP2K), 16, voff, 0, 0, 0);
     }
   };
-  // step s's A22 tile of this wave in accumulator layout (gathered through the pair's permutation: one
-  // row-table read per row, no search); and its store from the accumulators.  The lane's half-row
-  // offset 4h is laundered so that what depends on it is formed per step, not held in registers
-  // across the loop; row offsets 8q + r ride in the scalar offset of each buffer access.
-  const unsigned N4 = 4u * (unsigned)N;
-  auto issueC = [&](int s, floatx16& c) {
+  // 4 of a step's 16 A22 loads, gathered (one row-table read per row, no search)
+  auto issueCQ = [&](int s, floatx16& c, int q) {
     int h4 = 4 * h;
     asm volatile("" : "+v"(h4));
-    const int* rt = rowsrc + kD2S * s + 32 * wr + h4;
-    const unsigned cc4 = 4u * (unsigned)min(col, N - 1);
+    const int* rt = rowsrc + kD2S * s + h4;
+    const unsigned cc4 = 4u * (unsigned)colc;
 #pragma unroll
-    for (int v = 0; v < 16; ++v) {
-      const unsigned src = (unsigned)rt[8 * (v >> 2) + (v & 3)];
-      c[v] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(IADMM_RS, __umul24(src, N4) + cc4, 0, 0));
+    for (int r = 0; r < 4; ++r) {
+      const unsigned src = (unsigned)rt[8 * q + r];
+      c[4 * q + r] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(IADMM_RS, __umul24(src, N4) + cc4, 0, 0));
     }
   };
-  auto storeC = [&](int s, const floatx16& c) {
-    int h4 = 4 * h;
-    asm volatile("" : "+v"(h4));
-    // rows >= N land past the matrix's end, columns >= N on an offset past it: dropped either way
-    const unsigned vb = col < N ? (unsigned)((c0 + kD2S * s + 32 * wr + h4) * N + col) * 4u : kOut;
-#pragma unroll
-    for (int v = 0; v < 16; ++v)
-      // (__float_as_uint on a copy: hipcc 7.2 lowers __builtin_bit_cast of an ext-vector element
-      // reached through a reference to element 0 for every v -- all 16 stores wrote c[0])
-      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(float(c[v])), IADMM_RS, vb,
-                                            (int)((8 * (v >> 2) + (v & 3)) * N4), 0);
-  };
-  auto chain = [&](int s, const floatx16& c) -> floatx16 {
-    const float* lrow = Ls0 + (s & 1) * (kD2S * kP2K) + (32 * wr + il) * kP2K + (kR2 / 2) * h;
-    floatx16 acc = c;
-    float4 fa[kR2 / 8];
-    __builtin_amdgcn_sched_barrier(0);
-    fa[0] = *reinterpret_cast<const float4*>(lrow);
-    fa[1] = *reinterpret_cast<const float4*>(lrow + 4);
-#pragma unroll
-    for (int sg = 0; sg < kR2 / 8; ++sg) {
-      if (sg + 2 < kR2 / 8) fa[sg + 2] = *reinterpret_cast<const float4*>(lrow + 4 * (sg + 2));
-#pragma unroll
-      for (int s4 = 0; s4 < 4; ++s4) acc = mfma(get4(fa[sg], s4), get4(ub[sg], s4), acc);
-    }
-    __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
-#pragma unroll
-    for (int sg = 0; sg < kR2 / 8 - 2; ++sg) {
-      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-      __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
-    }
-    __builtin_amdgcn_sched_group_barrier(0x008, 8, 0);
-    __builtin_amdgcn_sched_barrier(0);
-    return acc;
-  };
-  // step s: (top) every memory operation so far has completed -- this step's L21 everywhere (the
-  // barrier), its A22 in registers, and the previous step's stores, so the next loads may reuse their
-  // registers; issue step s + 1's L21 and A22; the 128-MFMA chain; store.
-  auto body = [&](int s, floatx16& cc, floatx16& cn) {
+  // step s -- cc: A22 (s) in, result (s) out; co: result (s - 1), stored; cn: A22 (s + 1), loaded
+  auto body = [&](int s, floatx16& cc, const floatx16& co, floatx16& cn) {
     vm_wait<0>();
-    __syncthreads();
-    issueL(s + 1);  // (past the last step: clamped rows, never used)
-    issueC(s + 1, cn);
-    cc = chain(s, cc);
-    storeC(s, cc);
+    __syncthreads();  // L21 (s) everywhere; every wave past chain (s - 1): ring slot (s + 1) & 1 free
+    const float* lrow = Ls0 + (s & 1) * (kD2S * kP2K) + il * kP2K + 4 * h;
+    const unsigned la = (unsigned)(uintptr_t)(const __attribute__((address_space(3))) float*)lrow;
+    typedef float f4v __attribute__((ext_vector_type(4)));
+    f4v fa[kR2 / 8];  // fragment g = 4j + q: L21[row il][32j + 8q + 4h + 0..3], at byte offset 32 g
+    floatx16 acc = cc;
+    asm volatile("ds_read_b128 %0, %1" : "=v"(fa[0]) : "v"(la));
+    asm volatile("ds_read_b128 %0, %1 offset:32" : "=v"(fa[1]) : "v"(la));
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int g = 0; g < kR2 / 8; ++g) {
+      if (g + 2 < kR2 / 8) asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(fa[g + 2]) : "v"(la), "i"(32 * (g + 2)));
+      // fa[g] landed (LDS operations complete in order; the other work of a group waits for its own)
+      if (g + 2 < kR2 / 8) asm volatile("s_waitcnt lgkmcnt(2)" : "+v"(fa[g]));
+      else if (g + 1 < kR2 / 8) asm volatile("s_waitcnt lgkmcnt(1)" : "+v"(fa[g]));
+      else asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(fa[g]));
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        if (!kNoMfma) acc = mfma(fa[g][r], u[g >> 2][4 * (g & 3) + r], acc);
+        else acc[r] = fmaf(fa[g][r], u[g >> 2][4 * (g & 3) + r], acc[r]);  // (hipcc 7.2 crashes on an empty chain)
+      }
+      if (!kNoMem && g >= 1 && g < 5) issueCQ(s + 1, cn, g - 1);
+      if (!kNoMem && g >= 5 && g < 9) issueLQ(s + 1, g - 5);
+      if (!kNoMem && g >= 9 && g < 13) storeQ(s - 1, co, g - 9);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    cc = acc;
   };
-  floatx16 cA, cB;
-  issueL(0);
-  issueC(0, cA);
+  floatx16 cA, cB, cX = {};  // (cX: the first step's "previous result", its stores dropped)
+#pragma unroll
+  for (int q = 0; q < 4; ++q) issueLQ(0, q);
+#pragma unroll
+  for (int q = 0; q < 4; ++q) issueCQ(0, cA, q);
   int s = 0;
-  for (; s + 1 < nsteps; s += 2) {
-    body(s, cA, cB);
-    body(s + 1, cB, cA);
+  for (; s + 2 < nsteps; s += 3) {
+    body(s, cA, cX, cB);
+    body(s + 1, cB, cA, cX);
+    body(s + 2, cX, cB, cA);
   }
-  if (s < nsteps) body(s, cA, cB);
+  // the last one or two steps, then the last result's stores
+  if (s + 1 < nsteps) {
+    body(s, cA, cX, cB);
+    body(s + 1, cB, cA, cX);
+    if (!kNoMem)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) storeQ(s + 1, cB, q);
+  } else if (s < nsteps) {
+    body(s, cA, cX, cB);
+    if (!kNoMem)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) storeQ(s, cA, q);
+  } else if (!kNoMem) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) storeQ(s - 1, cX, q);
+  }
   vm_wait<0>();
   __syncthreads();  // every gathered load of a pair row has completed: U12 to the pair's rows
-  if (wr == 0 && col < N) {
+  if (col < N) {
 #pragma unroll
-    for (int sg = 0; sg < kR2 / 8; ++sg) {
-      const int i = (kR2 / 2) * h + 4 * sg;
-      float* dst = Ab + (size_t)(P + i) * N + col;
-      dst[0] = -ub[sg].x;
-      dst[(size_t)N] = -ub[sg].y;
-      dst[2 * (size_t)N] = -ub[sg].z;
-      dst[3 * (size_t)N] = -ub[sg].w;
-    }
+    for (int j = 0; j < 8; ++j)
+#pragma unroll
+      for (int v = 0; v < 16; ++v) Ab[(size_t)(P + 32 * j + 8 * (v >> 2) + 4 * h + (v & 3)) * N + col] = -u[j][v];
   }
 }
 #undef IADMM_RS
@@ -1972,7 +1977,7 @@ static int lu_factor_blocks(int64_t B, int64_t N, float* A, int* piv, int* info,
   IADMM_ALLOW_LDS(lu_trail_kernel<false>, kTrailLds);
   IADMM_ALLOW_LDS(lu_trail128_kernel<true>, kT2Lds);
   IADMM_ALLOW_LDS(lu_trail128_kernel<false>, kT2Lds);
-  IADMM_ALLOW_LDS(lu_trail256_kernel, kP2Lds);
+  IADMM_ALLOW_LDS(lu_trail256_kernel<0>, kP2Lds);
   // defer: the interchanges left of each block wait for one final pass (lu_left_*_kernel); every
   // block keeps its permutation in a slot of its own until then
   const bool defer = gather && N <= kLeftDeferMaxN;
@@ -2066,7 +2071,7 @@ static int lu_factor_blocks(int64_t B, int64_t N, float* A, int* piv, int* info,
     const float* lv0 = linv + ((t + nbuf - 1) % nbuf) * B * (int64_t)kLinvFloats;  // block t - 1's (pairs)
     auto trail = [&](hipStream_t st, int tc0, int cnt) {
       const dim3 grid((unsigned)(B * cnt));
-      if (second) hipLaunchKernelGGL(lu_trail256_kernel, grid, dim3(kD2Threads), kP2Lds, st, (int)N, Pp, cnt, tc0, A, lv0, lv, pperm, pm);
+      if (second) hipLaunchKernelGGL(lu_trail256_kernel<0>, grid, dim3(kD2Threads), kP2Lds, st, (int)N, Pp, cnt, tc0, A, lv0, lv, pperm, pm);
       else if (vec) hipLaunchKernelGGL(lu_trail128_kernel<true>, grid, dim3(kT2Threads), kT2Lds, st, (int)N, P, cnt, tc0, A, lv, gp);
       else hipLaunchKernelGGL(lu_trail128_kernel<false>, grid, dim3(kT2Threads), kT2Lds, st, (int)N, P, cnt, tc0, A, lv, gp);
     };
