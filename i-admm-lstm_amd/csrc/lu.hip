@@ -1981,11 +1981,12 @@ static int lu_factor_blocks(int64_t B, int64_t N, float* A, int* piv, int* info,
   // defer: the interchanges left of each block wait for one final pass (lu_left_*_kernel); every
   // block keeps its permutation in a slot of its own until then
   const bool defer = gather && N <= kLeftDeferMaxN;
-  // paired blocks (r05, opt-in IADMM_LU_PAIRS, with defer and 16-B rows): block t (even) updates only
-  // block t + 1's columns, then one rank-256 update (lu_trail256_kernel) takes everything right of
-  // block t + 1 for both.  Measured slower than the rank-128 default (82.7 vs 78.4 ms at B = 1024,
-  // N = 2000, profiles/r05_lu_paired_*): the rank-256 kernel runs one workgroup per CU and reaches
-  // the rank-128 kernel's rate, not the MFMA ceiling, and every other block loses its look-ahead.
+  // paired blocks (r05, the default with defer and 16-B rows; IADMM_LU_RANK128 turns them off): block t
+  // (even) updates only block t + 1's columns, then one rank-256 update (lu_trail256_kernel) takes
+  // everything right of block t + 1 for both -- half the A22 traffic per flop.  At B = 1024, N = 2000:
+  // 75.7 ms on one stream vs 78.1 for rank-128 blocks with the look-ahead; with the look-ahead the
+  // paired form took 76.9 (the rank-256 update already fills the GPU, and the panels beside it slowed
+  // both), so paired factorizations run on the caller's stream (profiles/r05_lu_traces_v3.txt).
   const bool paired = pairs && defer && vec;
   const int nb = (int)((N + kOB - 1) / kOB);
   const int64_t slot = B * (int64_t)kPermInts;
@@ -1998,7 +1999,7 @@ static int lu_factor_blocks(int64_t B, int64_t N, float* A, int* piv, int* info,
   // end).  L11^-1 and (without defer) the block permutation alternate between two buffers.
   // (without a context, or with the interchanges as a pass of their own (gather = false), everything
   // runs in order on the caller's stream)
-  iadmm_lu_ctx* side = gather ? ctx : nullptr;
+  iadmm_lu_ctx* side = gather && !paired ? ctx : nullptr;
   if (side) {
     // Under stream capture every launch stays on the caller's stream (same factors, bit for bit):
     // capturing the fork / join across the context's two streams crashed the HIP 7.2 runtime in
@@ -2317,7 +2318,7 @@ extern "C" int iadmm_lu_factor_ex(int64_t B, int64_t N, float* A, int* piv, int*
                                   iadmm_lu_ctx* ctx, int flags, void* stream) {
   if (B <= 0 || N <= 0 || !A || !piv || !info || !ws) return IADMM_E_ARG;
   if (ws_bytes < lu_ws_bytes(B, N)) return IADMM_E_ARG;
-  if (flags & ~(IADMM_LU_FORCE_HBM | IADMM_LU_PAIRS)) return IADMM_E_ARG;
+  if (flags & ~(IADMM_LU_FORCE_HBM | IADMM_LU_PAIRS | IADMM_LU_RANK128)) return IADMM_E_ARG;
   if (!aligned16(ws)) return IADMM_E_ALIGN;
   if (N > kLuMaxHbmN || B > 0x7fffffff) return IADMM_E_SIZE;
   const int64_t ntc_max = (N + kTC - 1) / kTC, nrc_max = (N + kTRW - 1) / kTRW;
@@ -2337,7 +2338,7 @@ extern "C" int iadmm_lu_factor_ex(int64_t B, int64_t N, float* A, int* piv, int*
   float* linv = reinterpret_cast<float*>(static_cast<char*>(ws) + lu_perm_bytes(B, N) + lu_sig_bytes(B, N) +
                                          lu_pair_bytes(B, N));
   const bool gather = N <= kLuMaxN && !(flags & IADMM_LU_FORCE_HBM);
-  const bool pairs = (flags & IADMM_LU_PAIRS) != 0;
+  const bool pairs = !(flags & IADMM_LU_RANK128);
   return lu_factor_blocks(B, N, A, piv, info, perm, sig, pperm, linv, s, gather, pairs, ctx);
 }
 

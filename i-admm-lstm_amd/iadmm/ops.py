@@ -276,7 +276,8 @@ def lu_factor_ws(B, N, device):
 
 
 LU_FORCE_HBM = 1  # include/iadmm.h IADMM_LU_FORCE_HBM (tests)
-LU_PAIRS = 2      # include/iadmm.h IADMM_LU_PAIRS (opt-in rank-256 paired-block updates: A/B and tests)
+LU_PAIRS = 2      # include/iadmm.h IADMM_LU_PAIRS (rank-256 paired-block updates: the default since r05)
+LU_RANK128 = 4    # include/iadmm.h IADMM_LU_RANK128 (the r04 rank-128 blocks with the look-ahead: A/B and tests)
 
 
 class LuContext:
@@ -315,9 +316,9 @@ def lu_context():
 def lu_factor(K, ws=None, lookahead=True, flags=0):
     """In-place batched LU with partial pivoting: returns (LU (= K), piv int32 [B,N] 1-based (LAPACK), info int32 [B]).
     ``ws``: a :func:`lu_factor_ws` buffer (allocated per call when omitted).  ``lookahead``: factor the
-    next block beside each trailing update on this caller's :func:`lu_context` (N <= 2048; the
-    factors are bit for bit the same either way).  ``flags``: 0, :data:`LU_FORCE_HBM` and/or :data:`LU_PAIRS`
-    (tests / A/B)."""
+    next block beside each trailing update on this caller's :func:`lu_context` (rank-128 blocks: N > 2048
+    or :data:`LU_RANK128`; the factors are bit for bit the same either way).  ``flags``: 0,
+    :data:`LU_FORCE_HBM`, :data:`LU_RANK128` (tests / A/B); :data:`LU_PAIRS` is the default."""
     if K.dim() != 3 or K.shape[1] != K.shape[2]:
         raise ValueError(f"K must be [B,N,N], got {tuple(K.shape)}")
     B, N = K.shape[0], K.shape[1]

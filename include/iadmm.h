@@ -130,12 +130,15 @@ int iadmm_kkt_rhs(int64_t B, int64_t n, int64_t m, int64_t num_ineq, const float
  * every launch on `stream` (the cross-stream fork / join crashed the HIP 7.2 runtime at capture end).
  * A context belongs to the device current at its creation (IADMM_E_ARG on another) and serves one
  * factorization at a time in its streams' order: give each concurrent caller (thread / stream) its own.
- * flags: 0, or IADMM_LU_FORCE_HBM (tests: the forms for N above the LDS-table limits -- the
- * interchange pass instead of the gathered loads -- at any N), and/or IADMM_LU_PAIRS (opt-in, N <= 2048,
- * N % 4 == 0: two 128-column blocks share one rank-256 update of the columns right of them -- measured
- * slower than the default rank-128 updates, kept for study; different rounding, same accuracy). */
+ * Block pairs (r05, the default for N <= 2048 with N % 4 == 0 and 16-B aligned rows): two 128-column
+ * blocks share one rank-256 update of the columns right of them; these sizes run every launch on
+ * `stream` (the look-ahead measured slower there: the rank-256 update fills the GPU by itself).
+ * flags: 0, or any of IADMM_LU_FORCE_HBM (tests: the forms for N above the LDS-table limits -- the
+ * interchange pass instead of the gathered loads -- at any N), IADMM_LU_RANK128 (one rank-128 update
+ * per block at every N, with the look-ahead: the r04 form; different rounding, same accuracy),
+ * IADMM_LU_PAIRS (accepted for compatibility: the default since r05). */
 typedef struct iadmm_lu_ctx iadmm_lu_ctx;
-enum { IADMM_LU_FORCE_HBM = 1, IADMM_LU_PAIRS = 2 };
+enum { IADMM_LU_FORCE_HBM = 1, IADMM_LU_PAIRS = 2, IADMM_LU_RANK128 = 4 };
 int iadmm_lu_ctx_create(iadmm_lu_ctx** ctx);   /* on the current device; *ctx = NULL on failure */
 int iadmm_lu_ctx_destroy(iadmm_lu_ctx* ctx);   /* waits for the context's streams; NULL is a no-op */
 int64_t iadmm_lu_factor_ws_bytes(int64_t B, int64_t N);

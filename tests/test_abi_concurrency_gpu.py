@@ -3,11 +3,13 @@ stream-ordered calls that are safe to capture in a hipGraph and to call from sev
 distinct streams, and run-to-run determinism of the kernels whose stores go through LDS stages.
 
 * Stage II (models/lu.py:26-35): ``ops.lu_factor`` + ``ops.lu_solve`` captured with
-  ``torch.cuda.graph`` and replayed (the look-ahead context's fork / join across its two streams
-  becomes part of the graph) -- factors, pivots and solutions bitwise those of eager runs;
+  ``torch.cuda.graph`` and replayed (under capture every launch stays on the capturing stream) --
+  factors, pivots and solutions bitwise those of eager runs (N = 2000 paired blocks; N = 2500 rank-128
+  blocks, whose eager run uses the look-ahead);
 * two Python threads factoring different batches on two streams at the same time, each with its own
   look-ahead context -- bitwise the serial results;
-* the look-ahead (context) path bitwise equal to the single-stream path (NULL context);
+* the look-ahead (context) path bitwise equal to the single-stream path (NULL context), for the
+  paired-block default and for IADMM_LU_RANK128;
 * repeat runs bitwise equal: the LU at N = 2000, B = 4 (look-ahead + LDS-staged panels), and the
   cell backward (its dP stores staged through LDS, csrc/train.hip) at the config-5 width.
 """
@@ -36,9 +38,9 @@ def _kkt_like(B, N, seed):
     return K.cuda(), torch.randn(B, N, generator=g).cuda()
 
 
-def _factor_solve(K, b, lookahead=True):
+def _factor_solve(K, b, lookahead=True, flags=0):
     from iadmm import ops
-    LU, piv, info = ops.lu_factor(K.clone(), lookahead=lookahead)
+    LU, piv, info = ops.lu_factor(K.clone(), lookahead=lookahead, flags=flags)
     x = ops.lu_solve(LU, piv, b)
     return LU, piv, info, x
 
@@ -59,11 +61,16 @@ def _diff(a, b):
 
 
 @pytest.mark.timeout(300)
-def test_lu_repeat_and_lookahead_bitwise():
+@pytest.mark.parametrize("rank128", [False, True])
+def test_lu_repeat_and_lookahead_bitwise(rank128):
+    """N = 2000: the paired-block default (one stream) and the rank-128 blocks (look-ahead on the
+    context's streams)."""
+    from iadmm import ops
+    fl = ops.LU_RANK128 if rank128 else 0
     K, b = _kkt_like(4, 2000, 11)
-    r0 = _factor_solve(K, b)
-    r1 = _factor_solve(K, b)
-    r2 = _factor_solve(K, b, lookahead=False)
+    r0 = _factor_solve(K, b, flags=fl)
+    r1 = _factor_solve(K, b, flags=fl)
+    r2 = _factor_solve(K, b, lookahead=False, flags=fl)
     torch.cuda.synchronize()
     assert int(r0[2].abs().max()) == 0
     assert _same(r0, r1), ("LU not deterministic across runs", _diff(r0, r1))
@@ -71,9 +78,11 @@ def test_lu_repeat_and_lookahead_bitwise():
 
 
 @pytest.mark.timeout(300)
-def test_lu_graph_capture_replay_bitwise():
+@pytest.mark.parametrize("N", [2000, 2500])
+def test_lu_graph_capture_replay_bitwise(N):
+    """N = 2000: paired blocks; N = 2500: rank-128 blocks, whose eager run forks the look-ahead."""
     from iadmm import ops
-    B, N = 4, 2000
+    B = 4
     K, b = _kkt_like(B, N, 12)
     eager = _factor_solve(K, b)
     torch.cuda.synchronize()
@@ -110,7 +119,7 @@ def test_lu_graph_capture_replay_bitwise():
 
 @pytest.mark.timeout(300)
 def test_lu_two_threads_two_streams_bitwise():
-    ins = [_kkt_like(8, 2000, 20 + i) for i in range(2)]
+    ins = [_kkt_like(8, 2500, 20 + i) for i in range(2)]  # (N > 2048: rank-128 blocks, look-ahead contexts)
     serial = [_factor_solve(K, b) for K, b in ins]
     torch.cuda.synchronize()
     out = [None, None]

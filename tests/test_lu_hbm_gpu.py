@@ -10,7 +10,8 @@ through both forms, so they are pinned against
 the LDS-resident forms at sizes that have both:
 
 * factor: the same arithmetic in the same order, only the interchanges move elsewhere -> the factors
-  and pivots must be bit for bit those of the gathered form;
+  and pivots must be bit for bit those of the gathered form (both with rank-128 blocks,
+  IADMM_LU_RANK128: the paired-block default exists only in the gathered form);
 * solve: another summation order -> its distance to the fp64 solution within 2x the LDS-resident
   solve's own distance (+ 1e-6 relative: a random Gaussian matrix's condition number reaches 1e4 and
   more, so both are ~cond x eps away from it; N = 1101 measured 5e-5 between the two), and the
@@ -36,7 +37,8 @@ def _gpu():
 
 def _factor_solve(K, b, force):
     from iadmm import ops
-    flags = ops.LU_FORCE_HBM if force else 0
+    # (rank-128 blocks on both sides: the paired-block default needs the gathered form, N <= 2048)
+    flags = (ops.LU_FORCE_HBM if force else 0) | ops.LU_RANK128
     LU, piv, info = ops.lu_factor(K.clone(), flags=flags)
     x = ops.lu_solve(LU, piv, b, flags=flags & ops.LU_FORCE_HBM)
     torch.cuda.synchronize()

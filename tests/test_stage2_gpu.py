@@ -185,9 +185,9 @@ def test_kkt_assemble_bitwise(n, m):
 
 @pytest.mark.parametrize("N,B", [(2000, 3), (1024, 2), (516, 2)])
 def test_paired_blocks_match_rank128_form(N, B):
-    """Paired blocks (r05, opt-in IADMM_LU_PAIRS, csrc/lu.hip lu_trail256_kernel: one rank-256 update of
-    the columns right of every two 128-column blocks, the pair's interchanges composed into one gather)
-    against the default rank-128-per-block form on the same KKT-like matrices: a different summation
+    """Paired blocks (r05, the default for N <= 2048, csrc/lu.hip lu_trail256_kernel: one rank-256 update
+    of the columns right of every two 128-column blocks, the pair's interchanges composed into one gather)
+    against the rank-128-per-block form (IADMM_LU_RANK128) on the same KKT-like matrices: a different summation
     order, so not bitwise -- the backward errors ||PLU - K|| / ||K|| stay within
     1.5x of each other, and both solves land within 2x of each other's distance to the fp64 solution.
     N = 516: an odd block count with a partial last block (the last pair is a single block)."""
@@ -206,7 +206,7 @@ def test_paired_blocks_match_rank128_form(N, B):
     K = K.cuda()
     b = torch.randn(B, N, generator=g).cuda()
     res = {}
-    for name, fl in (("paired", ops.LU_PAIRS), ("rank128", 0)):
+    for name, fl in (("paired", 0), ("rank128", ops.LU_RANK128)):
         LU, piv, info = ops.lu_factor(K.clone(), flags=fl)
         x = ops.lu_solve(LU, piv, b)
         torch.cuda.synchronize()

@@ -87,7 +87,7 @@ def main():
     ap.add_argument("--N", type=int, default=2000)
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--child", action="store_true")
-    ap.add_argument("--flags", type=int, default=0, help="iadmm_lu_factor_ex flags (2 = IADMM_LU_PAIRS)")
+    ap.add_argument("--flags", type=int, default=0, help="iadmm_lu_factor_ex flags (4 = IADMM_LU_RANK128: the r04 form)")
     args = ap.parse_args()
     if args.child:
         return child(args)

@@ -13,7 +13,7 @@ import torch  # noqa: E402
 ap = argparse.ArgumentParser()
 ap.add_argument("--batch", type=int, default=1024)
 ap.add_argument("--N", type=int, default=2000)
-ap.add_argument("--flags", type=int, default=0, help="iadmm_lu_factor_ex flags (2 = IADMM_LU_PAIRS)")
+ap.add_argument("--flags", type=int, default=0, help="iadmm_lu_factor_ex flags (4 = IADMM_LU_RANK128: the r04 form)")
 ap.add_argument("--no-lookahead", action="store_true", help="every launch on one stream (clean durations)")
 a = ap.parse_args()
 from iadmm import data, ops  # noqa: E402
