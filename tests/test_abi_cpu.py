@@ -138,6 +138,6 @@ def test_lu_context_abi():
         _abi.call("iadmm_lu_ctx_create", None)
     need = lib.iadmm_lu_factor_ws_bytes(2, 100)
     with pytest.raises(_abi.IadmmError, match="bad argument"):  # unknown flag bits
-        _abi.call("iadmm_lu_factor_ex", 2, 100, 16, 16, 16, 16, need, None, 4, None)
+        _abi.call("iadmm_lu_factor_ex", 2, 100, 16, 16, 16, 16, need, None, 8, None)
     with pytest.raises(_abi.IadmmError, match="bad argument"):
         _abi.call("iadmm_lu_solve_ex", 2, 100, 16, 16, 16, 2, None)
