@@ -124,8 +124,7 @@ constexpr size_t kTrailLds = trail_lds<kTC>();
 // i / 64): per interchange a ballot search over the live slots and lane-indexed reads and writes,
 // no LDS round trip (r04: the LDS-resident lists cost ~500 cycles per interchange, ~30 us for a
 // 128-row block); the lists go to LDS once at the end.  The caller moves each column with all loads
-// before all stores, one memory latency instead of n.  NS = 4: a block (n <= 128); NS = 8: a pair of
-// blocks (n <= 256, r05 lu_pair_perm_kernel).
+// before all stores, one memory latency instead of n.  NS = 4: a block (n <= 128); NS = 8: n <= 256.
 // (wave: the wave that builds; sync = false: no closing barrier -- only that wave reads the lists)
 template <int NS = 4>
 IADMM_DEV void build_row_perm(const int* pv, int base, int n, int* rowid, int* cur, int* cnt, int wave = 0,
@@ -1340,37 +1339,21 @@ __global__ __launch_bounds__(kT2Threads, 2) void lu_trail128_kernel(int N, int P
 //         multipliers in block t + 1's rows);
 //   A22 -= [L21_t  L21_{t+1}] U12   (rank 256: 64 flop/B, MFMA-bound).
 // Interchanges: the far columns have had neither block's applied -- A22 and A12 rows gather through the
-// pair's composed permutation (lu_pair_perm_kernel: the pair's 256 pivots in order); block t's columns
+// pair's composed permutation (both blocks' own permutations composed); block t's columns
 // have had block t + 1's interchanges deferred too, so L21_t rows gather through block t + 1's own
 // permutation.  A displaced row's source is always one of the pair's 256 block rows, which take U12
 // only after the last step's loads (as in lu_trail128_kernel).
 constexpr int kR2 = 2 * kOB;                 // rank of the paired update
 constexpr int kP2K = kR2 + 4;                // LDS stride (k) of its L21 tiles and staged L rows
-constexpr int kPairMax = kR2;                // interchanges of a pair
-constexpr int kPairInts = 4 * kPairMax + 1;  // rowid[512], cur[512], cnt
 constexpr int kD2Threads = 256;              // lu_trail256_kernel: 4 waves, two workgroups per CU,
 constexpr int kD2S = 32;                     //   rows per step,
 constexpr int kD2Rows = 2048 + 2 * kD2S;     //   row-source table (N <= 2048, whole steps + one)
 constexpr int kP2BitWords = (2048 + 31) / 32 + 4;  // one per step (pairing only with the deferred left pass)
 constexpr int kP2AreaFloats = 2 * kD2S * kP2K;     // the L21 ring (two steps) = the prologue's 64 staged L rows
 constexpr size_t kP2Lds = (size_t)kP2AreaFloats * sizeof(float) +
-                          (size_t)(kPairMax + kD2Rows + 3 * kPermMax + kP2BitWords) * sizeof(int) +
+                          (size_t)(kR2 + kD2Rows + 3 * kPermMax + kP2BitWords) * sizeof(int) +
                           (size_t)((kP2BitWords + 3) & ~3);
 static_assert(2 * kP2Lds <= 160 * 1024, "two workgroups per CU (gfx950 LDS)");
-
-// one wave per instance: the composed permutation of the pair's 256 interchanges (rows [P, P + 256))
-__global__ __launch_bounds__(64) void lu_pair_perm_kernel(int N, int P, const int* piv, int* pperm) {
-  __shared__ int pvs[kPairMax], prow[2 * kPairMax], pcur[2 * kPairMax], pcnt[1];
-  const int lane = threadIdx.x;
-  const size_t b = blockIdx.x;
-  for (int i = lane; i < kPairMax; i += 64) pvs[i] = piv[b * N + P + i] - 1;
-  __syncthreads();
-  build_row_perm<8>(pvs, P, kPairMax, prow, pcur, pcnt, 0, false);
-  int* out = pperm + b * kPairInts;
-  const int cnt = *pcnt;
-  for (int i = lane; i < 2 * kPairMax; i += 64) { out[i] = i < cnt ? prow[i] : 0; out[2 * kPairMax + i] = i < cnt ? pcur[i] : 0; }
-  if (lane == 0) out[4 * kPairMax] = cnt;
-}
 
 // The paired far update: per (instance, 128-column strip right of the pair), all rows below it.  r05
 // third form: TWO workgroups of four waves per CU (2 waves per SIMD), 32-row steps, wave w owning the
@@ -1395,21 +1378,23 @@ __global__ __launch_bounds__(64) void lu_pair_perm_kernel(int N, int P, const in
 //             by inline-asm ds_read_b128 with explicit lgkmcnt waits: the compiler treats every LDS
 //             read as possibly aliasing an in-flight LDS-DMA and would drain vmcnt before it (the ring
 //             slot read is never the one the DMA fills).
-// Interchanges: A22 and A12 rows gather through the pair's composed permutation (pperm: a row-source
-// table, no search); L21's block-t half gathers through block t + 1's own permutation (perm1).  A
-// displaced row's source is one of the pair's 256 rows, which take U12 only after the last step's loads.
+// Interchanges: A22 and A12 rows gather through the pair's composed permutation -- a row-source table
+// over [P, N) composed in LDS at the start from the two blocks' own permutations (perm0, perm1: one
+// scatter each, no replay of the 256 pivots); L21's block-t half gathers through block t + 1's own
+// permutation.  A displaced row's source is one of the pair's 256 rows, which take U12 only after the
+// last step's loads.
 // Linv0 / Linv1: the two blocks' lu_linv_kernel buffers.  N % 4 == 0, 16-B aligned rows, N <= 2048
 // (the host checks).  MODE: tools/lubench256.hip's timing diagnostics only (results meaningless):
 // 4 = no main-loop memory work, 8 = one VALU op per main-loop MFMA instead, 16 = no prologue MFMAs.
 template <int MODE = 0>
 __global__ __launch_bounds__(kD2Threads, 2) void lu_trail256_kernel(int N, int P, int ntc, int tc0, float* A,
                                                                     const float* Linv0, const float* Linv1,
-                                                                    const int* pperm, const int* perm1) {
+                                                                    const int* perm0, const int* perm1) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   float* Ls0 = sm;                       // 2 x [32 rows][kP2K]: L21 of a step
   float* Lt = sm;                        // prologue: 64 staged L rows [64][kP2K]
-  int* bsrc = reinterpret_cast<int*>(sm + kP2AreaFloats);  // [256] source row of pair row P + i
-  int* rowsrc = bsrc + kPairMax;         // [kD2Rows] source row of row c0 + i (composed permutation)
+  int* bsrc = reinterpret_cast<int*>(sm + kP2AreaFloats);  // [256] source row of pair row P + i, then
+  int* rowsrc = bsrc + kR2;              // [kD2Rows] of row c0 + i (one table: the composed permutation)
   int* tdst1 = rowsrc + kD2Rows;         // [128] block t + 1's displaced rows,
   int* tsrc1 = tdst1 + kPermMax;         // [128] their sources,
   int* dsrc1 = tsrc1 + kPermMax;         // [128] sorted
@@ -1439,17 +1424,24 @@ __global__ __launch_bounds__(kD2Threads, 2) void lu_trail256_kernel(int N, int P
 #define IADMM_RS __builtin_amdgcn_make_buffer_rsrc(Abu, 0, N * N * 4, 0x00020000)
   const unsigned kOut = 0x7ffffff0u;     // an offset past the end: the store is dropped
 
-  // ---- the two permutations' tables
-  const int* pb = pperm + b * kPairInts;
+  // ---- the pair's row map, bsrc[x - P] (x in [P, c0 + kD2S (nsteps + 1))): the row whose content row x
+  // holds after both blocks' interchanges -- identity, then block t's (rowid -> cur), then block t + 1's
+  // on top (its sources read through the map before any of its writes); rows >= N clamped (the last
+  // step's look-ahead loads read one step past the end).  lu_block_perm layout: rowid [0, cnt), cur
+  // [256, 256 + cnt), cnt at 512.
+  const int* pa = perm0 + b * kPermInts;
   const int* qb = perm1 + b * kPermInts;
-  const int ndisp = pb[4 * kPairMax] - kR2, ndisp1 = qb[4 * kPermMax] - kOB;
-  for (int i = tid; i < kPairMax; i += NT) bsrc[i] = pb[2 * kPairMax + i];
+  const int cnta = pa[4 * kPermMax], ndisp1 = qb[4 * kPermMax] - kOB;
+  for (int x = tid; x < kR2 + kD2S * (nsteps + 1); x += NT) bsrc[x] = min(P + x, N - 1);
   if (tid < ndisp1) { tdst1[tid] = qb[kOB + tid]; tsrc1[tid] = qb[2 * kPermMax + kOB + tid]; }
   for (int w = tid; w < nsteps + 2; w += NT) { dbits1[w] = 0u; dpre1[w] = 0; }
-  for (int r = tid; r < kD2S * (nsteps + 1); r += NT) rowsrc[r] = min(c0 + r, N - 1);  // (>= N: clamped;
-  // one step past the end: the last step's look-ahead loads read it)
   __syncthreads();
-  for (int i = tid; i < ndisp; i += NT) rowsrc[pb[kR2 + i] - c0] = pb[2 * kPairMax + kR2 + i];  // (distinct rows)
+  for (int i = tid; i < cnta; i += NT) bsrc[pa[i] - P] = pa[2 * kPermMax + i];
+  __syncthreads();
+  const int cntb = ndisp1 + kOB;  // (<= 256 = NT)
+  const int vb1 = tid < cntb ? bsrc[qb[2 * kPermMax + tid] - P] : 0;
+  __syncthreads();
+  if (tid < cntb) bsrc[qb[tid] - P] = vb1;
   int drank1 = 0, dd1 = 0;
   if (tid < ndisp1) {
     dd1 = tdst1[tid] - c0;
@@ -1968,7 +1960,7 @@ struct iadmm_lu_ctx {
 
 static int lu_linv_bufs(int64_t N);
 
-static int lu_factor_blocks(int64_t B, int64_t N, float* A, int* piv, int* info, int* perm, int* sig, int* pperm,
+static int lu_factor_blocks(int64_t B, int64_t N, float* A, int* piv, int* info, int* perm, int* sig,
                             float* linv, hipStream_t s0, bool gather, bool pairs, iadmm_lu_ctx* ctx) {
   hipStream_t s = s0;
   const bool vec = (N % 4 == 0) && aligned16(A);
@@ -2065,14 +2057,10 @@ static int lu_factor_blocks(int64_t B, int64_t N, float* A, int* piv, int* info,
     const int Pp = second ? P - kOB : P;      // the update's own P (the pair's first row)
     const int ntc = ((int)N - c2 + kT2C - 1) / kT2C;
     const int* gp = gather ? pm : nullptr;
-    if (second) {
-      hipLaunchKernelGGL(lu_pair_perm_kernel, dim3((unsigned)B), dim3(64), 0, s, (int)N, Pp, piv, pperm);
-      LU_TRY_LAUNCH();
-    }
     const float* lv0 = linv + ((t + nbuf - 1) % nbuf) * B * (int64_t)kLinvFloats;  // block t - 1's (pairs)
     auto trail = [&](hipStream_t st, int tc0, int cnt) {
       const dim3 grid((unsigned)(B * cnt));
-      if (second) hipLaunchKernelGGL(lu_trail256_kernel<0>, grid, dim3(kD2Threads), kP2Lds, st, (int)N, Pp, cnt, tc0, A, lv0, lv, pperm, pm);
+      if (second) hipLaunchKernelGGL(lu_trail256_kernel<0>, grid, dim3(kD2Threads), kP2Lds, st, (int)N, Pp, cnt, tc0, A, lv0, lv, pm - slot, pm);
       else if (vec) hipLaunchKernelGGL(lu_trail128_kernel<true>, grid, dim3(kT2Threads), kT2Lds, st, (int)N, P, cnt, tc0, A, lv, gp);
       else hipLaunchKernelGGL(lu_trail128_kernel<false>, grid, dim3(kT2Threads), kT2Lds, st, (int)N, P, cnt, tc0, A, lv, gp);
     };
@@ -2266,14 +2254,11 @@ static int64_t lu_perm_bytes(int64_t B, int64_t N) {  // (two alternating slots 
 static int64_t lu_sig_bytes(int64_t B, int64_t N) {
   return N <= kLeftDeferMaxN ? al16(B * left_sig_off(N, lu_nb(N) - 1) * (int64_t)sizeof(int)) : 0;
 }
-static int64_t lu_pair_bytes(int64_t B, int64_t N) {  // the pair's composed permutation (paired blocks)
-  return N <= kLeftDeferMaxN ? al16(B * (int64_t)kPairInts * (int64_t)sizeof(int)) : 0;
-}
 static int lu_linv_bufs(int64_t N) {  // four with paired blocks, two with the look-ahead
   return N <= kLeftDeferMaxN ? 4 : (N <= kLuMaxN ? 2 : 1);
 }
 static int64_t lu_ws_bytes(int64_t B, int64_t N) {
-  return lu_perm_bytes(B, N) + lu_sig_bytes(B, N) + lu_pair_bytes(B, N) +
+  return lu_perm_bytes(B, N) + lu_sig_bytes(B, N) +
          lu_linv_bufs(N) * B * (int64_t)kLinvFloats * (int64_t)sizeof(float);
 }
 
@@ -2334,12 +2319,10 @@ extern "C" int iadmm_lu_factor_ex(int64_t B, int64_t N, float* A, int* piv, int*
   IADMM_CHECK_LAUNCH();
   int* perm = static_cast<int*>(ws);
   int* sig = reinterpret_cast<int*>(static_cast<char*>(ws) + lu_perm_bytes(B, N));
-  int* pperm = reinterpret_cast<int*>(static_cast<char*>(ws) + lu_perm_bytes(B, N) + lu_sig_bytes(B, N));
-  float* linv = reinterpret_cast<float*>(static_cast<char*>(ws) + lu_perm_bytes(B, N) + lu_sig_bytes(B, N) +
-                                         lu_pair_bytes(B, N));
+  float* linv = reinterpret_cast<float*>(static_cast<char*>(ws) + lu_perm_bytes(B, N) + lu_sig_bytes(B, N));
   const bool gather = N <= kLuMaxN && !(flags & IADMM_LU_FORCE_HBM);
   const bool pairs = !(flags & IADMM_LU_RANK128);
-  return lu_factor_blocks(B, N, A, piv, info, perm, sig, pperm, linv, s, gather, pairs, ctx);
+  return lu_factor_blocks(B, N, A, piv, info, perm, sig, linv, s, gather, pairs, ctx);
 }
 
 extern "C" int iadmm_lu_factor(int64_t B, int64_t N, float* A, int* piv, int* info, void* ws, int64_t ws_bytes,

@@ -19,14 +19,16 @@ __global__ void fill(float* p, int64_t n, float scale) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
     p[i] = scale * (1e-3f * (float)((i * 2654435761u) & 1023) - 0.5f);
 }
-// identity permutations of the pair (rows [Pp, Pp + 256)) and of its second block
-__global__ void ident(int64_t B, int Pp, int* pperm, int* perm1) {
+// identity permutations of the pair's two blocks (rows [Pp, Pp + 128) and [Pp + 128, Pp + 256))
+__global__ void ident(int64_t B, int Pp, int* perm0, int* perm1) {
   const int64_t b = blockIdx.x;
-  int* pb = pperm + b * kPairInts;
+  int* pa = perm0 + b * kPermInts;
   int* qb = perm1 + b * kPermInts;
-  for (int i = threadIdx.x; i < 2 * kPairMax; i += blockDim.x) { pb[i] = Pp + i; pb[2 * kPairMax + i] = Pp + i; }
-  for (int i = threadIdx.x; i < 2 * kPermMax; i += blockDim.x) { qb[i] = Pp + kOB + i; qb[2 * kPermMax + i] = Pp + kOB + i; }
-  if (threadIdx.x == 0) { pb[4 * kPairMax] = kR2; qb[4 * kPermMax] = kOB; }
+  for (int i = threadIdx.x; i < 2 * kPermMax; i += blockDim.x) {
+    pa[i] = pa[2 * kPermMax + i] = Pp + i;
+    qb[i] = qb[2 * kPermMax + i] = Pp + kOB + i;
+  }
+  if (threadIdx.x == 0) { pa[4 * kPermMax] = kOB; qb[4 * kPermMax] = kOB; }
 }
 }  // namespace iadmm
 using namespace iadmm;
@@ -63,7 +65,7 @@ int main(int argc, char** argv) {
   CK(hipMalloc(&A2, n * sizeof(float)));
   CK(hipMalloc(&L0, (size_t)B * kLinvFloats * sizeof(float)));
   CK(hipMalloc(&L1, (size_t)B * kLinvFloats * sizeof(float)));
-  CK(hipMalloc(&pp, (size_t)B * kPairInts * sizeof(int)));
+  CK(hipMalloc(&pp, (size_t)B * kPermInts * sizeof(int)));
   CK(hipMalloc(&p1, (size_t)B * kPermInts * sizeof(int)));
   hipLaunchKernelGGL(fill, dim3(8192), dim3(256), 0, 0, L0, (int64_t)B * kLinvFloats, 0.05f);
   hipLaunchKernelGGL(fill, dim3(8192), dim3(256), 0, 0, L1, (int64_t)B * kLinvFloats, 0.05f);
