@@ -1401,6 +1401,10 @@ __global__ __launch_bounds__(kD2Threads, 2) void lu_trail256_kernel(int N, int P
   unsigned* dbits1 = reinterpret_cast<unsigned*>(dsrc1 + kPermMax);  // one word per step
   unsigned char* dpre1 = reinterpret_cast<unsigned char*>(dbits1 + kP2BitWords);
   constexpr bool kNoMem = (MODE & 4) != 0, kNoMfma = (MODE & 8) != 0, kNoPro = (MODE & 16) != 0;
+  // where the memory work rides in the 32 fragment groups of a step's chain: the A22 loads of step s + 1
+  // in groups 2-5, its L21 DMA in 6-9, the stores of step s - 1 in 14, 17, 20, 23 (profiles/
+  // r05_lubench256_sched.txt: 1-4 / 5-8 / 9-12 was 1-4 % slower, other spreads within 1 %)
+  constexpr int kC0 = 2, kL0 = 6, kS0 = 14, kSs = 3;
   const int nwg = gridDim.x, bid = blockIdx.x;
   const int xcd = bid & 7, local = bid >> 3, q8 = nwg >> 3, r8 = nwg & 7;
   const int logical = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + local;
@@ -1582,9 +1586,9 @@ __global__ __launch_bounds__(kD2Threads, 2) void lu_trail256_kernel(int N, int P
         if (!kNoMfma) acc = mfma(fa[g][r], u[g >> 2][4 * (g & 3) + r], acc);
         else acc[r] = fmaf(fa[g][r], u[g >> 2][4 * (g & 3) + r], acc[r]);  // (hipcc 7.2 crashes on an empty chain)
       }
-      if (!kNoMem && g >= 1 && g < 5) issueCQ(s + 1, cn, g - 1);
-      if (!kNoMem && g >= 5 && g < 9) issueLQ(s + 1, g - 5);
-      if (!kNoMem && g >= 9 && g < 13) storeQ(s - 1, co, g - 9);
+      if (!kNoMem && g >= kC0 && g < kC0 + 4) issueCQ(s + 1, cn, g - kC0);
+      if (!kNoMem && g >= kL0 && g < kL0 + 4) issueLQ(s + 1, g - kL0);
+      if (!kNoMem && g >= kS0 && g < kS0 + 4 * kSs && (g - kS0) % kSs == 0) storeQ(s - 1, co, (g - kS0) / kSs);
       __builtin_amdgcn_sched_barrier(0);
     }
     cc = acc;

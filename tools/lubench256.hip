@@ -3,7 +3,8 @@
 // the diagnostic variants -- without the main loop's memory work (MODE 4), without its MFMAs (8: one
 // VALU op each instead), without the prologue's MFMAs (16), and with only the main loop's MFMAs
 // (4 + 16) -- on identity permutations (every row in place: the gathered addressing is still
-// exercised, through the identity tables).  Results of the diagnostic variants are meaningless.
+// exercised, through the identity tables).  Results of the diagnostic variants are meaningless (and
+// no-mem ones are void: the compiler drops the chain whose result is never stored).
 // (r05 second form, one 8-wave workgroup per CU: profiles/r05_lubench256.txt, in this file's history.)
 // Build: hipcc -O3 -std=c++17 --offload-arch=gfx950 tools/lubench256.hip -o tools/lubench256.bin
 #include "../i-admm-lstm_amd/csrc/lu.hip"
