@@ -284,7 +284,8 @@ def cpu_baseline(args, d, params, gpu_out, weights_tag, extra=()):
                           f"share of one GPU's lease (16); os.cpu_count() = {os.cpu_count()} counts the whole host",
                sample=f"{Bc} instances x full solve (Ruiz + K={args.outer_T} + unscale), the same synthetic "
                       f"instances 0..{Bc - 1} and weights ({weights_tag}) as the GPU run, {dt:.1f} s; "
-                      f"8 of config 1's 64 instances (CPU cost is linear in the batch)",
+                      + (f"{Bc} of config 1's 64 instances (CPU cost is linear in the batch; all 64 timed once: "
+                         "profiles/r05_cpu_leg_64.json)" if Bc < 64 else "all 64 of config 1's instances"),
                final_primal=float(out["primal"].mean()), final_dual=float(out["dual"].mean()),
                parity={weights_tag: parity(gpu_out, out, Bc)})
     for tag, prm, gout in extra:
