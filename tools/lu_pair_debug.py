@@ -1,5 +1,6 @@
-"""Debug helper (r05): factor one small matrix with and without IADMM_LU_PAIRS and report where the
-packed factors differ (by 64 x 64 region), to localise a fault in the paired rank-256 update."""
+"""Debug helper (r05): factor one small matrix with the paired-block default and with IADMM_LU_RANK128
+and report where the packed factors differ (by 64 x 64 region), to localise a fault in the paired
+rank-256 update."""
 import os
 import sys
 
@@ -11,11 +12,11 @@ N = int(sys.argv[1]) if len(sys.argv) > 1 else 384
 g = torch.Generator().manual_seed(5)
 K = (torch.randn(1, N, N, generator=g) + 4 * torch.eye(N)).cuda()  # diagonally heavy: few interchanges
 out = {}
-for fl in (0, ops.LU_PAIRS):
+for fl in (ops.LU_RANK128, 0):
     LU, piv, info = ops.lu_factor(K.clone(), flags=fl, lookahead=False)
     torch.cuda.synchronize()
     out[fl] = (LU[0].cpu(), piv[0].cpu(), int(info[0]))
-a, b = out[0], out[ops.LU_PAIRS]
+a, b = out[ops.LU_RANK128], out[0]
 print("info", a[2], b[2], "piv equal", torch.equal(a[1], b[1]), "first piv diff", (a[1] != b[1]).nonzero()[:3].flatten().tolist())
 d = (a[0] - b[0]).abs()
 for r0 in range(0, N, 64):
