@@ -5,7 +5,7 @@ scope of main.py:825-834,881-890,1024-1031): Ruiz scaling (10 rounds) -> K=100 S
 iterations -> final unscale.  Instances: n=1000, 500 inequality + 500 equality rows, hidden 800,
 B=1024 per GPU (synthetic, restating generate_data.py:67-76).  Weights: the checkpoint
 ``checkpoints/QP_{n}_{eq}_{ineq}_{T}_{h}.pth`` (main.py's naming; the reference's own training recipe,
-scripts/Synthetic.sh:3, run through this repo's main.py train mode -- the epoch-55 save, adopted in
+scripts/Synthetic.sh:3, run through this repo's main.py train mode -- the epoch-61 save, adopted in
 r05 after passing the K = 100 fp64 envelope, checkpoints/README.md) when it exists, else random init
 with the reference's initialisation.  Throughput does not depend on weight values; the final residual does (the
 random-init solve diverges at this shape), so both are reported when a checkpoint is used.
