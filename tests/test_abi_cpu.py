@@ -141,3 +141,14 @@ def test_lu_context_abi():
         _abi.call("iadmm_lu_factor_ex", 2, 100, 16, 16, 16, 16, need, None, 8, None)
     with pytest.raises(_abi.IadmmError, match="bad argument"):
         _abi.call("iadmm_lu_solve_ex", 2, 100, 16, 16, 16, 2, None)
+
+
+def test_lu_flag_constants_match_header():
+    """ops' LU flag constants are the header's enum values (IADMM_LU_PAIRS is the default since r05,
+    IADMM_LU_RANK128 selects the r04 rank-128 form)."""
+    import re
+    from iadmm import ops
+    hdr = open(HEADER).read()
+    enum = dict((k, int(v)) for k, v in re.findall(r"(IADMM_LU_\w+)\s*=\s*(\d+)", hdr))
+    assert enum == {"IADMM_LU_FORCE_HBM": ops.LU_FORCE_HBM, "IADMM_LU_PAIRS": ops.LU_PAIRS,
+                    "IADMM_LU_RANK128": ops.LU_RANK128}
