@@ -1,7 +1,7 @@
 // ADMM scalar schedule and the fused x/z/y update.
 //
 // Reference: models/lstm.py:60-63 (rho, rho_vec, alpha), :80 (+ b_h), :82-94 (xv step, x
-// relaxation, z projection, dual update); models/lu.py:133-140 (Stage II variant with z
+// relaxation, z projection, dual update); models/lu.py:38-45 (Stage II variant with z
 // relaxation).  Compiled with -ffp-contract=off so every a*b+c below rounds twice, exactly as
 // the reference's separate tensor ops do.
 #include "common.h"

@@ -563,7 +563,7 @@ __global__ __launch_bounds__(kKktThreads) void kkt_matvec_kernel(KktArgs a, cons
   }
 }
 
-// Dense K (models/lstm.py:67-68, models/lu.py:123-124) for Stage II and explicit inspection.
+// Dense K (models/lstm.py:67-68, models/lu.py:28-29) for Stage II and explicit inspection.
 // One 64 x 64 tile of K per workgroup (blockIdx.x = instance, blockIdx.y = tile): rows of K are
 // written as coalesced 256-B segments; the A0^T block is staged through LDS so that A0 is also read
 // along its rows (a direct per-element formula read it with stride n and ran at 1.3 TB/s).

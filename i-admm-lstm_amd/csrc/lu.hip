@@ -1761,7 +1761,7 @@ __global__ void lu_info_zero_kernel(int64_t B, int* info) {
   if (i < B) info[i] = 0;
 }
 
-// b~ = [sigma x - p ; z - y / rho]  (models/lu.py:125,129)
+// b~ = [sigma x - p ; z - y / rho]  (models/lu.py:30,34)
 __global__ void kkt_rhs_kernel(int64_t B, int n, int m, int num_ineq, const float* p, const float* x,
                                const float* y, const float* z, float sigma, const float* scal,
                                const float* rho_rows, float* out) {

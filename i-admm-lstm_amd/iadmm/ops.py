@@ -160,7 +160,7 @@ def lstm_cell_f16x3(H16, C, xv, g, Upk16, wscale, Wx, Hn16=None, Cn=None, part=N
 # --------------------------------------------------------------------------- ADMM update
 def admm_update(n, m, num_ineq, part, b_h, xv, x, y, z, zl, zu, scal, relax_z=False, out=None,
                 rho_vec=None, rho_rows=None):
-    """xv' / x' / z' / y' (models/lstm.py:80-94; relax_z -> models/lu.py:133-140)."""
+    """xv' / x' / z' / y' (models/lstm.py:80-94; relax_z -> models/lu.py:38-45)."""
     B = x.shape[0]
     if out is None:
         out = (torch.empty_like(xv), torch.empty_like(x), torch.empty_like(y), torch.empty_like(z))
@@ -260,7 +260,7 @@ def kkt_assemble(Q, A0, sigma, scal, num_ineq, rho_rows=None):
 
 
 def kkt_rhs(p, x, y, z, sigma, scal=None, num_ineq=0, rho_rows=None, out=None):
-    """b~ = [sigma x - p ; z - y / rho], [B,n+m] (models/lu.py:125)."""
+    """b~ = [sigma x - p ; z - y / rho], [B,n+m] (models/lu.py:30)."""
     B, n = x.shape[0], x.shape[1]
     m = y.shape[1]
     out = empty(B, n + m, like=x) if out is None else out

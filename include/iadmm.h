@@ -99,13 +99,13 @@ int iadmm_kkt_matvec(int64_t B, int64_t n, int64_t m, int64_t num_ineq, const fl
                      const float* A0, const float* v, float sigma, const float* scal,
                      const float* rho_rows, int transpose, float* out, void* stream);
 
-/* Dense K[B,n+m,n+m] (models/lstm.py:67-68, models/lu.py:123-124): for Stage II and tests.
+/* Dense K[B,n+m,n+m] (models/lstm.py:67-68, models/lu.py:28-29): for Stage II and tests.
  * rho from ``scal`` (two classes) or per row from ``rho_rows`` [B,m] when non-NULL. */
 int iadmm_kkt_assemble(int64_t B, int64_t n, int64_t m, int64_t num_ineq, const float* Q,
                        const float* A0, float sigma, const float* scal, const float* rho_rows,
                        float* K, void* stream);
 
-/* b~ = [sigma x - p ; z - y / rho] (models/lu.py:125,129) into out[B,n+m]; rho as above. */
+/* b~ = [sigma x - p ; z - y / rho] (models/lu.py:30,34) into out[B,n+m]; rho as above. */
 int iadmm_kkt_rhs(int64_t B, int64_t n, int64_t m, int64_t num_ineq, const float* p,
                   const float* x, const float* y, const float* z, float sigma,
                   const float* scal, const float* rho_rows, float* out, void* stream);
@@ -115,12 +115,14 @@ int iadmm_kkt_rhs(int64_t B, int64_t n, int64_t m, int64_t num_ineq, const float
  * (row i was swapped with row piv[i]-1);
  * info[B] = first 1-based zero pivot or 0.  Right-looking in 128-column blocks (two 64-column halves; 16-column
  * panels up to N = 2048, 8-column panels on 1024-thread workgroups above, held in registers up to 10240 panel
- * rows and in HBM beyond; rank-128 MFMA trailing update with the block's interchanges as gathered loads up to
- * N = 36736, as a pass of their own above; limit N <= 46340, N * N < 2^31).
+ * rows and in HBM beyond; fp32-MFMA trailing updates -- rank 256 per pair of blocks at N <= 2048, rank 128
+ * above -- with the block's interchanges as gathered loads up to N = 36736, as a pass of their own above;
+ * limit N <= 46340, N * N < 2^31).
  * N <= 2048 (r04): the interchanges left of each block are applied once at the end.
  * ws: caller-owned, 16-B aligned device workspace of at least iadmm_lu_factor_ws_bytes(B, N) bytes
  * (per-instance block permutations -- one per 128-column block for N <= 2048, with the composed
- * left permutations, two for N <= 36736 -- and the 128x128 two-level L11^-1 blocks, two for N <= 36736);
+ * left permutations, two for N <= 36736 -- and the 128x128 two-level L11^-1 blocks, four for N <= 2048,
+ * two for N <= 36736);
  * nothing is allocated inside.
  * iadmm_lu_factor runs every launch in order on `stream`.  iadmm_lu_factor_ex with a context (N <= 36736)
  * factors the next block beside the rest of each trailing update (look-ahead) on the context's two
@@ -205,7 +207,7 @@ int iadmm_lstm_cell_fwd_f16x3(int64_t M, int64_t h, const void* H16, const float
 /* ADMM update (replaces models/lstm.py:80 ``+ b_h`` and :82-94):
  * grad = sum_tiles part + b_h ; xv' = xv - grad ; x' = alpha xv'[:n] + (1-alpha) x ;
  * z~ = z + (v - y)/rho ; z' = clamp(z~ + y/rho, zl, zu) ; y' = y + rho (z~ - z').
- * relax_z != 0 applies alpha to z as well (models/lu.py:138, Stage II); then ``part`` is NULL
+ * relax_z != 0 applies alpha to z as well (models/lu.py:43, Stage II); then ``part`` is NULL
  * and ``xv`` already holds the solved xv'.  ``rho_rows`` [B,m] (optional) overrides the two-class
  * rho of ``scal`` per row (the explicit rho_vec of models/lu.py:13).  Outputs must not alias
  * inputs. rho_vec (optional output) receives the rho used per row. */

@@ -54,7 +54,7 @@ def kkt_matrix(Q, A0, sigma, rho_vec):
 
 
 def kkt_rhs(x, z, y, p, sigma, rho_vec):
-    """b~ = [sigma x - p ; z - y / rho_vec] (models/lstm.py:69, models/lu.py:125)."""
+    """b~ = [sigma x - p ; z - y / rho_vec] (models/lstm.py:69, models/lu.py:30)."""
     return torch.cat((sigma * x - p, z - (1 / rho_vec) * y), dim=1)
 
 
@@ -78,12 +78,12 @@ def lstm_cell(params, inputs, H, C):
 
 
 def admm_relax_project(xv_new, x, y, z, zl, zu, rho_vec, alpha, relax_z=False):
-    """x/z/y updates shared by both stages (models/lstm.py:84-94, models/lu.py:133-140)."""
+    """x/z/y updates shared by both stages (models/lstm.py:84-94, models/lu.py:38-45)."""
     n = x.shape[1]
     x_t, v = xv_new[:, :n, :], xv_new[:, n:, :]
     z_t = z + (1 / rho_vec) * (v - y)
     x_out = alpha * x_t + (1 - alpha) * x
-    z_rel = alpha * z_t + (1 - alpha) * z if relax_z else z_t  # lstm.py:91-92 vs lu.py:138
+    z_rel = alpha * z_t + (1 - alpha) * z if relax_z else z_t  # lstm.py:91-92 vs lu.py:43
     z_out = torch.max(torch.min(z_rel + (1 / rho_vec) * y, zu), zl)
     y_out = y + rho_vec * (z_rel - z_out)
     return x_out, y_out, z_out
