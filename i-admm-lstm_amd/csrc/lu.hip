@@ -2266,9 +2266,10 @@ static int64_t lu_ws_bytes(int64_t B, int64_t N) {
          lu_linv_bufs(N) * B * (int64_t)kLinvFloats * (int64_t)sizeof(float);
 }
 
+// (+ 64 B: the two half-batch workspaces of a split factorization round up separately)
 extern "C" int64_t iadmm_lu_factor_ws_bytes(int64_t B, int64_t N) {
   if (B <= 0 || N <= 0) return 0;
-  return lu_ws_bytes(B, N);
+  return lu_ws_bytes(B, N) + 64;
 }
 
 extern "C" int iadmm_lu_ctx_create(iadmm_lu_ctx** out) {
@@ -2321,12 +2322,43 @@ extern "C" int iadmm_lu_factor_ex(int64_t B, int64_t N, float* A, int* piv, int*
   hipStream_t s = (hipStream_t)stream;
   hipLaunchKernelGGL(lu_info_zero_kernel, dim3((unsigned)((B + 255) / 256)), dim3(256), 0, s, B, info);
   IADMM_CHECK_LAUNCH();
-  int* perm = static_cast<int*>(ws);
-  int* sig = reinterpret_cast<int*>(static_cast<char*>(ws) + lu_perm_bytes(B, N));
-  float* linv = reinterpret_cast<float*>(static_cast<char*>(ws) + lu_perm_bytes(B, N) + lu_sig_bytes(B, N));
   const bool gather = N <= kLuMaxN && !(flags & IADMM_LU_FORCE_HBM);
   const bool pairs = !(flags & IADMM_LU_RANK128);
-  return lu_factor_blocks(B, N, A, piv, info, perm, sig, linv, s, gather, pairs, ctx);
+  auto run = [&](int64_t b0, int64_t nb, char* w, hipStream_t st, iadmm_lu_ctx* c) {
+    int* perm = reinterpret_cast<int*>(w);
+    int* sig = reinterpret_cast<int*>(w + lu_perm_bytes(nb, N));
+    float* linv = reinterpret_cast<float*>(w + lu_perm_bytes(nb, N) + lu_sig_bytes(nb, N));
+    return lu_factor_blocks(nb, N, A + b0 * N * N, piv + b0 * N, info + b0, perm, sig, linv, st, gather, pairs, c);
+  };
+  // Batch split (r05): the paired-block form runs on one stream (no look-ahead), so with a context and a
+  // batch of at least two instances per CU the two halves are factored concurrently on the context's
+  // two streams -- the instances share nothing, so the factors are bit for bit those of one call, and
+  // one half's latency-bound panel steps overlap the other half's updates (B = 1024, N = 2000: 75.8 ->
+  // 74.1 ms, profiles/r05_lu_split_ab.txt; four parts: 78.7).  Not under stream capture (see below).
+  bool split = ctx && pairs && gather && N <= kLeftDeferMaxN && N % 4 == 0 && aligned16(A) && B >= 512 &&
+               ws_bytes >= lu_ws_bytes(B / 2, N) + lu_ws_bytes(B - B / 2, N);
+  if (split) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    IADMM_HIP_RC(hipStreamIsCapturing(s, &cs));
+    split = cs == hipStreamCaptureStatusNone;
+  }
+  if (!split) return run(0, B, static_cast<char*>(ws), s, ctx);
+  const int64_t B0 = B / 2, B1 = B - B0;
+  char* w1 = static_cast<char*>(ws) + lu_ws_bytes(B0, N);  // (16-B multiple)
+  IADMM_HIP_RC(hipEventRecord(ctx->ev0, s));
+  IADMM_HIP_RC(hipStreamWaitEvent(ctx->s1, ctx->ev0, 0));
+  IADMM_HIP_RC(hipStreamWaitEvent(ctx->s2, ctx->ev0, 0));
+  // from here on both streams are joined back into s whatever fails
+  int rc = run(0, B0, static_cast<char*>(ws), ctx->s1, nullptr);
+  const int rc1 = run(B0, B1, w1, ctx->s2, nullptr);
+  if (!rc) rc = rc1;
+  hipError_t e = hipEventRecord(ctx->ev1, ctx->s1);
+  if (e == hipSuccess) e = hipStreamWaitEvent(s, ctx->ev1, 0);
+  if (e != hipSuccess && !rc) rc = (int)e;
+  e = hipEventRecord(ctx->join, ctx->s2);
+  if (e == hipSuccess) e = hipStreamWaitEvent(s, ctx->join, 0);
+  if (e != hipSuccess && !rc) rc = (int)e;
+  return rc;
 }
 
 extern "C" int iadmm_lu_factor(int64_t B, int64_t N, float* A, int* piv, int* info, void* ws, int64_t ws_bytes,

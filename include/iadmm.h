@@ -133,8 +133,10 @@ int iadmm_kkt_rhs(int64_t B, int64_t n, int64_t m, int64_t num_ineq, const float
  * A context belongs to the device current at its creation (IADMM_E_ARG on another) and serves one
  * factorization at a time in its streams' order: give each concurrent caller (thread / stream) its own.
  * Block pairs (r05, the default for N <= 2048 with N % 4 == 0 and 16-B aligned rows): two 128-column
- * blocks share one rank-256 update of the columns right of them; these sizes run every launch on
- * `stream` (the look-ahead measured slower there: the rank-256 update fills the GPU by itself).
+ * blocks share one rank-256 update of the columns right of them; no look-ahead there (measured slower:
+ * the rank-256 update fills the GPU by itself); instead, with a context and B >= 512, the two halves
+ * of the batch are factored concurrently on the context's streams (forked from and joined back into
+ * `stream`), bit for bit the one-stream factors.
  * flags: 0, or any of IADMM_LU_FORCE_HBM (tests: the forms for N above the LDS-table limits -- the
  * interchange pass instead of the gathered loads -- at any N), IADMM_LU_RANK128 (one rank-128 update
  * per block at every N, with the look-ahead: the r04 form; different rounding, same accuracy),

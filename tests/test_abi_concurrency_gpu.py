@@ -9,7 +9,8 @@ distinct streams, and run-to-run determinism of the kernels whose stores go thro
 * two Python threads factoring different batches on two streams at the same time, each with its own
   look-ahead context -- bitwise the serial results;
 * the look-ahead (context) path bitwise equal to the single-stream path (NULL context), for the
-  paired-block default and for IADMM_LU_RANK128;
+  paired-block default and for IADMM_LU_RANK128, and the batch split over the context's two streams
+  (B >= 512) bitwise equal to one stream;
 * repeat runs bitwise equal: the LU at N = 2000, B = 4 (look-ahead + LDS-staged panels), and the
   cell backward (its dP stores staged through LDS, csrc/train.hip) at the config-5 width.
 """
@@ -115,6 +116,18 @@ def test_lu_graph_capture_replay_bitwise(N):
     g.replay()
     torch.cuda.synchronize()
     assert _same((LU, piv, info, x), ref2), _diff((LU, piv, info, x), ref2)
+
+
+@pytest.mark.timeout(300)
+def test_lu_batch_split_bitwise():
+    """B >= 512 at N <= 2048 with a context: the two halves (256 + 257 here) are factored on the
+    context's two streams (csrc/lu.hip iadmm_lu_factor_ex) -- bitwise the one-stream factorization."""
+    K, b = _kkt_like(513, 2000, 31)
+    split = _factor_solve(K, b)
+    one = _factor_solve(K, b, lookahead=False)
+    torch.cuda.synchronize()
+    assert int(split[2].abs().max()) == 0
+    assert _same(split, one), ("batch-split factorization differs from one stream", _diff(split, one))
 
 
 @pytest.mark.timeout(300)
