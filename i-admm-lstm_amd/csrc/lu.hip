@@ -2307,7 +2307,7 @@ extern "C" int iadmm_lu_ctx_destroy(iadmm_lu_ctx* c) {
 extern "C" int iadmm_lu_factor_ex(int64_t B, int64_t N, float* A, int* piv, int* info, void* ws, int64_t ws_bytes,
                                   iadmm_lu_ctx* ctx, int flags, void* stream) {
   if (B <= 0 || N <= 0 || !A || !piv || !info || !ws) return IADMM_E_ARG;
-  if (ws_bytes < lu_ws_bytes(B, N)) return IADMM_E_ARG;
+  if (ws_bytes < lu_ws_bytes(B, N) + 64) return IADMM_E_ARG;  // (= iadmm_lu_factor_ws_bytes)
   if (flags & ~(IADMM_LU_FORCE_HBM | IADMM_LU_PAIRS | IADMM_LU_RANK128)) return IADMM_E_ARG;
   if (!aligned16(ws)) return IADMM_E_ALIGN;
   if (N > kLuMaxHbmN || B > 0x7fffffff) return IADMM_E_SIZE;
