@@ -1,6 +1,7 @@
 """Experiment (r05): the batched LU at B = 1024, N = 2000 as one call on one stream against the batch split
 into k equal parts factored concurrently on k streams (no data is shared between instances).  Prints the
 best of a few reps for each, and whether the factors are bitwise the same.
+Parts 0 is the library's own split (iadmm_lu_factor_ex with a context, r05).
     python tools/lu_split_ab.py [--parts 2 4] [--reps 4]"""
 import argparse
 import os
@@ -33,8 +34,8 @@ def run(parts):
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     cur = torch.cuda.current_stream()
     e0.record()
-    if parts == 1:
-        LU, piv, info = ops.lu_factor(K, ws=ws[1][0], lookahead=False)
+    if parts in (0, 1):  # 1: one stream (no context); 0: the library's own split (context, B >= 512)
+        LU, piv, info = ops.lu_factor(K, ws=ws[1][0], lookahead=parts == 0)
         outs = [(piv, info)]
     else:
         outs = []
@@ -56,7 +57,7 @@ def run(parts):
 streams = [torch.cuda.Stream() for _ in range(max(a.parts))]
 ws = {p: [ops.lu_factor_ws(B // p, N, "cuda") for _ in range(p)] for p in [1] + a.parts}
 res = {}
-for p in [1] + a.parts:
+for p in [1, 0] + a.parts:
     run(p)
     ts = []
     for _ in range(a.reps):
@@ -64,4 +65,4 @@ for p in [1] + a.parts:
         ts.append(t)
     res[p] = (min(ts), fp, ps)
     print(f"parts {p}: best {min(ts):.2f} ms (reps {', '.join(f'{t:.2f}' for t in ts)}), fingerprint {fp} piv {ps}", flush=True)
-print("bitwise equal to one call:", {p: res[p][1:] == res[1][1:] for p in a.parts})
+print("bitwise equal to one call:", {p: res[p][1:] == res[1][1:] for p in [0] + a.parts}, "(parts 0 = the library's split)")
