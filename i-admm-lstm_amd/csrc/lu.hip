@@ -1491,6 +1491,11 @@ __global__ __launch_bounds__(kD2Threads, 2) void lu_trail256_kernel(int N, int P
     const float* src = lane < 32 ? lo_src + 4 * lane : hi_src + 4 * (lane - 32);
     __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)(Lt + r * kP2K), 16, 0, 0);
   };
+  // every gathered A12 row of the prologue in flight at once (one memory latency, not four)
+#pragma unroll
+  for (int j = 0; j < 8; ++j)
+#pragma unroll
+    for (int v = 0; v < 16; ++v) u[j][v] = Ab[(size_t)bsrc[32 * j + 8 * (v >> 2) + 4 * h + (v & 3)] * N + colc];
 #pragma unroll
   for (int ph = 0; ph < 4; ++ph) {
     // pair rows [64 ph, 64 ph + 64): block t's rows hold Linv0 (columns [0, 128); the high half-row a
@@ -1505,10 +1510,6 @@ __global__ __launch_bounds__(kD2Threads, 2) void lu_trail256_kernel(int N, int P
         stage_row(r, Ab + (size_t)qb[2 * kPermMax + pr - kOB] * N + P, Linv1 + b * (size_t)kLinvFloats + (size_t)(pr - kOB) * kOB);
       }
     }
-#pragma unroll
-    for (int j = 2 * ph; j < 2 * ph + 2; ++j)
-#pragma unroll
-      for (int v = 0; v < 16; ++v) u[j][v] = Ab[(size_t)bsrc[32 * j + 8 * (v >> 2) + 4 * h + (v & 3)] * N + colc];
     vm_wait<0>();
     __syncthreads();
     if (!kNoPro) {
