@@ -183,3 +183,30 @@ def test_cell_backward_repeat_bitwise():
     torch.cuda.synchronize()
     assert all(bool(torch.isfinite(t).all()) for t in r0)
     assert _same(r0, r1), "cell backward not deterministic across runs"
+
+
+@pytest.mark.timeout(300)
+def test_lu_bench_shape_repeat_bitwise():
+    """the bench's Stage-II shape (B = 1024, N = 2000: paired rank-256 blocks, the
+    batch split over the context's two streams, every CU holding two co-resident workgroups of each
+    LDS-staged kernel) factored twice in one process -- factors, pivots and info bitwise equal; and
+    once more on one stream (NULL context), bitwise equal too."""
+    from iadmm import ops
+    B, N = 1024, 2000
+    g = torch.Generator(device="cuda").manual_seed(21)
+    K = torch.randn(B, N, N, generator=g, device="cuda")
+    K[:, 0, 0] = 0.0
+    ws = ops.lu_factor_ws(B, N, K.device)
+    outs = []
+    for lookahead in (True, True, False):
+        A = K.clone()
+        LU, piv, info = ops.lu_factor(A, ws=ws, lookahead=lookahead)
+        torch.cuda.synchronize()
+        outs.append((LU, piv.clone(), info.clone()))
+        del A
+    assert int(outs[0][2].abs().max()) == 0
+    for i in (1, 2):
+        if not _same(outs[0], outs[i]):
+            bad = (outs[0][0] != outs[i][0]).flatten(1).any(1).nonzero().flatten().tolist()
+            pytest.fail(f"run {i} differs from run 0 on {len(bad)} instances (first {bad[:8]}): "
+                        f"{_diff(outs[0], outs[i])}")

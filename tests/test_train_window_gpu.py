@@ -11,11 +11,23 @@ parameter (stated before measuring):
 
     rel-L2(grad_HIP - grad_fp64) <= 2 x rel-L2(grad_fp32 oracle - grad_fp64) + 1e-7.
 
-Two weight sets: the reference's initialisation (models/lstm.py:21-41, seed 17) and the same
-weights x 6 (gates away from their linear regime, larger rho / alpha excursions).  (r05 first tried
-x 20: that drives the solve into a chaotic regime -- loss 4e4 -- where the fp32 oracle's gradient is
-2.5e-3 from fp64 on the GPU's instances and 1.6 (i.e. uncorrelated) on the CPU generator's, and any two
-fp32 orders of the same algorithm disagree by that much: a coin toss, not a test of the kernels.)
+Three weight sets: the reference's initialisation (models/lstm.py:21-41, seed 17), the same weights
+x 6 (gates away from their linear regime, larger rho / alpha excursions) and x 20.
+
+x 20 drives the solve into a chaotic regime (loss ~5e3): in r05 the HIP gradients
+of every U_* were 2.2-3.0x the fp32 oracle's fp64 distance.  Whether that is chaos or a kernel bias is
+measured here, per parameter, instead of asserted:
+
+    pert64 = rel-L2(grad_fp64(inputs and parameters each moved by one fp32 ulp, seeded signs) - grad_fp64)
+    pert32 = rel-L2(grad_fp32 oracle(same perturbed inputs) - grad_fp64)
+    chaos  = max(fp32 oracle vs fp64, pert64, pert32)
+
+and the x 20 bound is rel-L2(grad_HIP - grad_fp64) <= 2 x chaos + 1e-7 (the rule VERDICT r05 states);
+x 1 and x 6 keep the r05 bound against the fp32 oracle alone.  pert64 is the fp64 algorithm's own
+sensitivity to the representation error of its fp32 inputs: an fp32 implementation in any order
+cannot be expected closer to fp64 than the dynamics amplify one rounding.  (On the CPU generator's
+instances at x 20, pert64 is 40-150, i.e. one ulp decorrelates the gradient completely;
+`profiles/r06_train_window_chaos.txt` holds the GPU box's numbers.)
 """
 import os
 
@@ -37,6 +49,16 @@ def rel_l2(a, b):
     return float((a - b).norm() / max(float(b.norm()), 1e-30))
 
 
+def perturb_ulp(t, seed):
+    """Each finite element moved one fp32 ulp up or down (seeded sign); infinities kept."""
+    t = t.detach().cpu().float()
+    g = torch.Generator().manual_seed(seed)
+    up = torch.randint(0, 2, t.shape, generator=g).bool()
+    moved = torch.where(up, torch.nextafter(t, torch.full_like(t, float("inf"))),
+                        torch.nextafter(t, torch.full_like(t, -float("inf"))))
+    return torch.where(torch.isfinite(t), moved, t)
+
+
 def oracle_grads(params, d, dtype):
     prm = {k: v.detach().cpu().to(dtype).requires_grad_(True) for k, v in params.items()}
     Q, p, A0, zl, zu = (d[k].cpu().to(dtype) for k in ("Q", "p", "A0", "zl", "zu"))
@@ -55,7 +77,7 @@ def oracle_grads(params, d, dtype):
 
 
 @pytest.mark.timeout(600)
-@pytest.mark.parametrize("scale", [1.0, 6.0])
+@pytest.mark.parametrize("scale", [1.0, 6.0, 20.0])
 def test_full_window_grads_fp64_envelope(scale):
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
@@ -87,20 +109,31 @@ def test_full_window_grads_fp64_envelope(scale):
     try:
         l32, g32 = oracle_grads(params, d, torch.float32)
         l64, g64 = oracle_grads(params, d, torch.float64)
+        pparams = {k: perturb_ulp(v, i) for i, (k, v) in enumerate(params.items())}
+        pd = {k: perturb_ulp(v, 100 + i) for i, (k, v) in enumerate(d.items())}
+        lp64, gp64 = oracle_grads(pparams, pd, torch.float64)
+        lp32, gp32 = oracle_grads(pparams, pd, torch.float32)
     finally:
         torch.set_num_threads(threads)
+    chaotic = scale >= 20.0
     lerr, lerr32 = abs(float(loss) - l64), abs(l32 - l64)
+    lchaos = max(lerr32, abs(lp64 - l64), abs(lp32 - l64)) if chaotic else lerr32
     report, bad = {}, {}
     for k, prm in model.named_parameters():
         assert prm.grad is not None and bool(torch.isfinite(prm.grad).all()), k
         e64 = rel_l2(prm.grad, g64[k])
         o64 = rel_l2(g32[k], g64[k])
+        p64 = rel_l2(gp64[k], g64[k])
+        p32 = rel_l2(gp32[k], g64[k])
         e32 = rel_l2(prm.grad, g32[k])
-        report[k] = (e64, o64, e32)
-        if e64 > FACTOR * o64 + FLOOR:
+        bound = FACTOR * (max(o64, p64, p32) if chaotic else o64) + FLOOR
+        report[k] = (e64, o64, p64, p32, e32, e64 / bound)
+        if e64 > bound:
             bad[k] = report[k]
-    print(f"[T=100 window grads x{scale:g}] loss {l64:.6e} (|HIP - fp64| {lerr:.1e}, |fp32 - fp64| {lerr32:.1e}); "
-          "per parameter (HIP vs fp64, fp32 oracle vs fp64, HIP vs fp32 oracle):",
+    print(f"[T=100 window grads x{scale:g}] loss {l64:.6e} (|HIP - fp64| {lerr:.1e}, |fp32 - fp64| {lerr32:.1e}, "
+          f"|fp64(1 ulp) - fp64| {abs(lp64 - l64):.1e}, |fp32(1 ulp) - fp64| {abs(lp32 - l64):.1e}); per parameter "
+          "(HIP vs fp64, fp32 oracle vs fp64, fp64(1 ulp) vs fp64, fp32(1 ulp) vs fp64, HIP vs fp32 oracle, "
+          f"HIP / bound; bound = {FACTOR:g} x {'max of the three' if chaotic else 'fp32 oracle'}):",
           {k: tuple(f"{v:.1e}" for v in r) for k, r in report.items()})
-    assert lerr <= FACTOR * lerr32 + FLOOR * abs(l64), (lerr, lerr32)
+    assert lerr <= FACTOR * lchaos + FLOOR * abs(l64), (lerr, lchaos)
     assert not bad, bad
