@@ -1525,6 +1525,13 @@ __global__ __launch_bounds__(kD2Threads, 2) void lu_trail256_kernel(int N, int P
   const unsigned N4 = 4u * (unsigned)N;
   // (the lane's half-row offset 4h is laundered so that what depends on it is formed per use, not held
   // in registers across the loop; row offsets 8q + r ride in the scalar offset of each buffer access)
+  // Stores past row N on a partial last step (N = 2000: rows 2000..2015 of the last 32-row step) are
+  // dropped by the descriptor's range check only because gfx950 counts the SGPR soffset in it
+  // (voffset + soffset >= num_records drops the access): measured on the box by
+  // tools/buffer_soffset_probe.hip, profiles/r04_buffer_soffset_probe.txt ("soffset IS part of the
+  // range check").  A target that excluded soffset would write the next instance's leading rows here;
+  // tests/test_abi_concurrency_gpu.py::test_lu_bench_shape_repeat_bitwise (N = 2000, every instance's
+  // factors and pivots) and the Stage-II envelope tests would catch that.
   auto storeQ = [&](int s, const floatx16& c, int q) {  // 4 of a step's 16 stores (s < 0: dropped)
     int h4 = 4 * h;
     asm volatile("" : "+v"(h4));
@@ -2259,8 +2266,12 @@ static int64_t lu_perm_bytes(int64_t B, int64_t N) {  // (two alternating slots 
 static int64_t lu_sig_bytes(int64_t B, int64_t N) {
   return N <= kLeftDeferMaxN ? al16(B * left_sig_off(N, lu_nb(N) - 1) * (int64_t)sizeof(int)) : 0;
 }
-static int lu_linv_bufs(int64_t N) {  // four with paired blocks, two with the look-ahead
-  return N <= kLeftDeferMaxN ? 4 : (N <= kLuMaxN ? 2 : 1);
+// Two alternating L11^-1 buffers: the look-ahead factors block t + 1 (writing its buffer) while block
+// t's update still reads the other; a paired update reads blocks t and t + 1's (both), and block t + 2
+// rewrites block t's only after that update, in order on the same stream (a batch split gives each half
+// its own workspace).  (r05 sized four for the paired form; ADVICE r05: nothing read them concurrently.)
+static int lu_linv_bufs(int64_t N) {
+  return N <= kLuMaxN ? 2 : 1;
 }
 static int64_t lu_ws_bytes(int64_t B, int64_t N) {
   return lu_perm_bytes(B, N) + lu_sig_bytes(B, N) +

@@ -9,8 +9,25 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-# IADMM_LIB_PATH: an alternative build of the same library (variant studies in tools/ only)
-LIB_PATH = os.environ.get("IADMM_LIB_PATH") or os.path.join(_HERE, "libiadmm.so")
+_REPO = os.path.dirname(os.path.dirname(_HERE))
+
+
+def _lib_path():
+    """The in-tree product library.  IADMM_LIB_PATH names an alternative build of the same library for
+    the variant studies of tools/ (tools/lu_ab.py, tools/cellbwd_ab.py, ...); it is honoured only for a
+    .so under the repository's tools/ or variants/ directory, so the product path cannot be swapped
+    for an arbitrary library."""
+    alt = os.environ.get("IADMM_LIB_PATH")
+    if not alt:
+        return os.path.join(_HERE, "libiadmm.so")
+    real = os.path.realpath(alt)
+    roots = [os.path.realpath(os.path.join(_REPO, d)) + os.sep for d in ("tools", "variants")]
+    if not real.endswith(".so") or not any(real.startswith(r) for r in roots):
+        raise RuntimeError(f"IADMM_LIB_PATH={alt!r}: variant libraries must be .so files under tools/ or variants/")
+    return real
+
+
+LIB_PATH = _lib_path()
 
 i64, f32, vp, cint = ctypes.c_int64, ctypes.c_float, ctypes.c_void_p, ctypes.c_int
 

@@ -299,17 +299,29 @@ class LuContext:
                 pass
 
 
-_LU_CTX = {}  # (device, caller stream, thread) -> LuContext: one per concurrent caller
+_LU_CTX = threading.local()  # per thread: OrderedDict (device, caller stream) -> LuContext
+LU_CTX_PER_THREAD = 8        # least recently used contexts beyond this are destroyed
 
 
 def lu_context():
     """The LuContext of the current (device, stream, thread): a context serves one factorization at a
     time in its streams' order, so concurrent callers -- other threads, other streams, a graph capture
-    beside eager work -- each get their own."""
-    key = (torch.cuda.current_device(), torch.cuda.current_stream().cuda_stream, threading.get_ident())
-    ctx = _LU_CTX.get(key)
+    beside eager work -- each get their own.  Held in thread-local storage (a finished thread's
+    contexts are destroyed with it) and at most LU_CTX_PER_THREAD per thread, least recently used
+    evicted (a caller on fresh streams no longer leaks HIP streams and events; destroying
+    a context waits for its streams' work, iadmm_lu_ctx_destroy)."""
+    import collections
+    cache = getattr(_LU_CTX, "map", None)
+    if cache is None:
+        cache = _LU_CTX.map = collections.OrderedDict()
+    key = (torch.cuda.current_device(), torch.cuda.current_stream().cuda_stream)
+    ctx = cache.get(key)
     if ctx is None:
-        ctx = _LU_CTX[key] = LuContext()
+        ctx = cache[key] = LuContext()
+        while len(cache) > LU_CTX_PER_THREAD:
+            cache.popitem(last=False)
+    else:
+        cache.move_to_end(key)
     return ctx
 
 

@@ -59,35 +59,48 @@ def ordered_reduce_grads(params, chunk_grads, dist, bucket_bytes=32 << 20):
     tensors (None = no gradient) aligned with ``params``.  Rank r's micro-batches follow rank r-1's
     in the global order (contiguous shards, parallel.shard).  A parameter that got no gradient in
     any micro-batch of any rank keeps ``grad = None``, as in one process (so Adam skips it instead
-    of applying weight decay and moment updates to a zero gradient): one small MAX all-reduce of a
-    per-parameter mask."""
+    of applying weight decay and moment updates to a zero gradient): a per-parameter count of the
+    micro-batches that produced a gradient rides at the end of the last bucket's fold (ADVICE r05:
+    no collective of its own)."""
     global ALLREDUCE_CALLS
     world, rank = dist.get_world_size(), dist.get_rank()
     params = list(params)
     if not params:
         return
     index = {id(p): i for i, p in enumerate(params)}
-    got = torch.tensor([float(any(g[i] is not None for g in chunk_grads)) for i in range(len(params))],
-                       device=params[0].device)
-    dist.all_reduce(got, op=dist.ReduceOp.MAX)
-    got = got.cpu().tolist()
-    for bucket in _buckets(params, bucket_bytes):
+    P = len(params)
+    ref0 = params[0]
+    mask = torch.tensor([float(sum(g[i] is not None for g in chunk_grads)) for i in range(P)],
+                        dtype=ref0.dtype, device=ref0.device)
+    buckets = _buckets(params, bucket_bytes)
+    totals = []
+    for bi, bucket in enumerate(buckets):
+        last = bi == len(buckets) - 1
         ids = [index[id(q)] for q in bucket]
         numel = sum(q.numel() for q in bucket)
+        extra = P if last else 0
         ref = bucket[0]
         acc = None
         if rank > 0:
-            acc = torch.empty(numel, dtype=ref.dtype, device=ref.device)
+            acc = torch.empty(numel + extra, dtype=ref.dtype, device=ref.device)
             dist.recv(acc, src=rank - 1)
         for g in chunk_grads:
             flat = torch.cat([(g[i] if g[i] is not None else torch.zeros_like(params[i])).reshape(-1) for i in ids])
-            acc = flat if acc is None else acc + flat
+            if acc is None:
+                acc = torch.cat([flat, torch.zeros(extra, dtype=ref.dtype, device=ref.device)]) if extra else flat
+            else:
+                acc[:numel] = acc[:numel] + flat
         if acc is None:  # rank 0 without instances (global batch < world)
-            acc = torch.zeros(numel, dtype=ref.dtype, device=ref.device)
+            acc = torch.zeros(numel + extra, dtype=ref.dtype, device=ref.device)
+        if extra:
+            acc[numel:] += mask
         if rank < world - 1:
             dist.send(acc, dst=rank + 1)
         dist.broadcast(acc, src=world - 1)
         ALLREDUCE_CALLS += 1
+        totals.append((bucket, acc))
+    got = totals[-1][1][-P:].cpu().tolist()  # (one D2H; the window's loss read syncs anyway)
+    for bucket, acc in totals:
         off = 0
         for q in bucket:
             if not got[index[id(q)]]:

@@ -121,8 +121,8 @@ int iadmm_kkt_rhs(int64_t B, int64_t n, int64_t m, int64_t num_ineq, const float
  * N <= 2048 (r04): the interchanges left of each block are applied once at the end.
  * ws: caller-owned, 16-B aligned device workspace of at least iadmm_lu_factor_ws_bytes(B, N) bytes
  * (per-instance block permutations -- one per 128-column block for N <= 2048, with the composed
- * left permutations, two for N <= 36736 -- and the 128x128 two-level L11^-1 blocks, four for N <= 2048,
- * two for N <= 36736);
+ * left permutations, two for N <= 36736 -- and the 128x128 two-level L11^-1 blocks, two for N <= 36736,
+ * one above);
  * nothing is allocated inside.
  * iadmm_lu_factor runs every launch in order on `stream`.  iadmm_lu_factor_ex with a context (N <= 36736)
  * factors the next block beside the rest of each trailing update (look-ahead) on the context's two

@@ -152,3 +152,20 @@ def test_lu_flag_constants_match_header():
     enum = dict((k, int(v)) for k, v in re.findall(r"(IADMM_LU_\w+)\s*=\s*(\d+)", hdr))
     assert enum == {"IADMM_LU_FORCE_HBM": ops.LU_FORCE_HBM, "IADMM_LU_PAIRS": ops.LU_PAIRS,
                     "IADMM_LU_RANK128": ops.LU_RANK128}
+
+
+def test_lib_path_override_limited_to_variant_dirs(tmp_path):
+    """IADMM_LIB_PATH (tools/ variant studies) cannot point the product path at an arbitrary library
+    (VERDICT r05 item 9)."""
+    import subprocess
+    import sys
+    bad = tmp_path / "libother.so"
+    bad.write_bytes(b"")
+    code = "import iadmm_path; from iadmm import _abi"
+    env = dict(os.environ, IADMM_LIB_PATH=str(bad))
+    r = subprocess.run([sys.executable, "-c", code], cwd=REPO, env=env, capture_output=True, text=True)
+    assert r.returncode != 0 and "tools/ or variants/" in r.stderr
+    env["IADMM_LIB_PATH"] = ""
+    r = subprocess.run([sys.executable, "-c", code + "; print(_abi.LIB_PATH)"], cwd=REPO, env=env,
+                       capture_output=True, text=True)
+    assert r.returncode == 0 and r.stdout.strip().endswith("iadmm/libiadmm.so"), r.stderr

@@ -183,14 +183,16 @@ def test_kkt_assemble_bitwise(n, m):
     assert torch.equal(torch.signbit(K.cpu()), torch.signbit(ref))
 
 
-@pytest.mark.parametrize("N,B", [(2000, 3), (1024, 2), (516, 2)])
+@pytest.mark.parametrize("N,B", [(2000, 3), (1024, 2), (516, 2), (1024, 512)])
 def test_paired_blocks_match_rank128_form(N, B):
     """Paired blocks (r05, the default for N <= 2048, csrc/lu.hip lu_trail256_kernel: one rank-256 update
     of the columns right of every two 128-column blocks, the pair's interchanges composed into one gather)
     against the rank-128-per-block form (IADMM_LU_RANK128) on the same KKT-like matrices: a different summation
     order, so not bitwise -- the backward errors ||PLU - K|| / ||K|| stay within
     1.5x of each other, and both solves land within 2x of each other's distance to the fp64 solution.
-    N = 516: an odd block count with a partial last block (the last pair is a single block)."""
+    N = 516: an odd block count with a partial last block (the last pair is a single block).
+    B = 512: the paired default then splits the batch over the context's two streams -- checked
+    against rank-128 as above and bitwise against the same factorization on one stream."""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     from iadmm import ops
@@ -217,6 +219,12 @@ def test_paired_blocks_match_rank128_form(N, B):
         x64 = torch.linalg.solve(Kd, b.double())
         ferr = (x.double() - x64).norm(dim=1) / x64.norm(dim=1)
         res[name] = (piv, berr, ferr)
+        if name == "paired" and B >= 512:
+            LU1, piv1, _ = ops.lu_factor(K.clone(), flags=fl, lookahead=False)
+            torch.cuda.synchronize()
+            assert torch.equal(LU1, LU) and torch.equal(piv1, piv), "batch split differs from one stream"
+            del LU1
+        del LU
     print(f"[paired N={N}] backward error paired {res['paired'][1].tolist()} rank-128 {res['rank128'][1].tolist()}; "
           f"forward error paired {res['paired'][2].tolist()} rank-128 {res['rank128'][2].tolist()}")
     # (no pivot comparison: a different summation order breaks near-ties in the pivot search, and one

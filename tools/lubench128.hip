@@ -491,7 +491,8 @@ __global__ __launch_bounds__(256, 2) void lu_trail128d_kernel(int N, int P, int 
     const int nval = min(kDRS, N - r0);
     const __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc(Ab + (size_t)r0 * N, 0, nval * N * 4, 0x00020000);
     const unsigned vb = cok ? ((unsigned)(4 * h) * (unsigned)N * 4u + (unsigned)col * 4u) : 0x80000000u;
-    if (nval == kDRS) {  // (the SGPR offset is outside the range check: full steps only)
+    if (nval == kDRS) {  // (full steps: the SGPR row offset; gfx950 does count soffset in the range check --
+                         //  profiles/r04_buffer_soffset_probe.txt -- but this bench keeps the r03 guard)
 #pragma unroll
       for (int rt = 0; rt < 2; ++rt)
 #pragma unroll
