@@ -130,9 +130,12 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(int64_t M, int Ni, int 
 // contiguous KiB) instead of row-major [Ni][K] (16 rows x 64 B per piece).
 // K16 (A_PACKED, K % 16 == 0): the VALU-free main loop (cell_tile.h mainloop_dma_k16), bitwise the
 // same products and order.
-template <bool ACC, bool A_PACKED, int NA, bool K16 = false>
-__global__ __launch_bounds__(256, 2) void gemm_nt_dma_kernel(int64_t M, int Ni, int K, const float* X,
-                                                             const float* W, float* out) {
+// The body: rows [r0, r0 + 256) x outputs [i0, i0 + TI) over the K range [k0, k0 + Klen) of the
+// Kfull-wide operands (k0 a multiple of 32; the whole K unless split), stored to out (+ its values
+// when ACC).
+template <bool ACC, bool A_PACKED, int NA, bool K16>
+IADMM_DEV void gemm_nt_dma_tile(int64_t M, int Ni, int Kfull, int k0, int Klen, const float* X, const float* W,
+                                float* out) {
   extern __shared__ __attribute__((aligned(16))) float ring[];
   constexpr int TI = NA * 32;
   const int nit = (Ni + TI - 1) / TI;
@@ -145,16 +148,16 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_dma_kernel(int64_t M, int Ni, 
   const int64_t r0 = rt * 256;
   floatx16 acc[NA][2];
   if constexpr (A_PACKED && K16) {
-    const int64_t nkc32 = (K + kBK - 1) / kBK;
-    mainloop_dma_k16<NA>(W + (int64_t)it * nkc32 * TI * kBK, X + r0 * K, M - r0, K, K, ring, acc, tid, wave, jl, hf,
-                         [] {});
+    const int64_t nkc32 = (Kfull + kBK - 1) / kBK;
+    mainloop_dma_k16<NA>(W + ((int64_t)it * nkc32 + k0 / kBK) * TI * kBK, X + r0 * Kfull + k0, M - r0, Kfull, Klen,
+                         ring, acc, tid, wave, jl, hf, [] {});
   } else if constexpr (A_PACKED) {
-    const int64_t nkc32 = (K + kBK - 1) / kBK;
-    mainloop_dma<true, NA>(W + (int64_t)it * nkc32 * TI * kBK, TI, kBK, X + r0 * K, M - r0, K, K, ring, acc, tid,
-                           wave, jl, hf, [] {});
+    const int64_t nkc32 = (Kfull + kBK - 1) / kBK;
+    mainloop_dma<true, NA>(W + (int64_t)it * nkc32 * TI * kBK, TI, kBK, X + r0 * Kfull, M - r0, Kfull, Kfull, ring,
+                           acc, tid, wave, jl, hf, [] {});
   } else {
-    mainloop_dma<false, NA>(W + (int64_t)i0 * K, Ni - i0, K, X + r0 * K, M - r0, K, K, ring, acc, tid, wave, jl,
-                            hf, [] {});
+    mainloop_dma<false, NA>(W + (int64_t)i0 * Kfull, Ni - i0, Kfull, X + r0 * Kfull, M - r0, Kfull, Kfull, ring,
+                            acc, tid, wave, jl, hf, [] {});
   }
 #pragma unroll
   for (int r = 0; r < 2; ++r) {
@@ -176,6 +179,24 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_dma_kernel(int64_t M, int Ni, 
         }
       }
   }
+}
+
+template <bool ACC, bool A_PACKED, int NA, bool K16 = false>
+__global__ __launch_bounds__(256, 2) void gemm_nt_dma_kernel(int64_t M, int Ni, int K, const float* X,
+                                                             const float* W, float* out) {
+  gemm_nt_dma_tile<ACC, A_PACKED, NA, K16>(M, Ni, K, 0, K, X, W, out);
+}
+
+// K split (r06, small M: the recipe's batch 2 has M = 4000 rows = 80 output tiles, a third of the
+// CUs): split blockIdx.y takes the K range [kpart * y, min(K, kpart * (y + 1))) (kpart % 32 == 0)
+// and writes its partial product to slab[y][M][Ni]; iadmm_slab_reduce sums the slabs in split
+// order.  Packed W, K % 16 == 0 (the VALU-free loop).
+template <int NA>
+__global__ __launch_bounds__(256, 2) void gemm_nt_dma_split_kernel(int64_t M, int Ni, int K, int kpart,
+                                                                   const float* X, const float* W, float* slab) {
+  const int k0 = kpart * (int)blockIdx.y;
+  const int klen = min(kpart, K - k0);
+  gemm_nt_dma_tile<false, true, NA, true>(M, Ni, K, k0, klen, X, W, slab + (int64_t)blockIdx.y * M * Ni);
 }
 
 // Output-tile height of the DMA gemm_nt: 160 rows when that pads Ni less than 128 rows would.
@@ -642,6 +663,38 @@ extern "C" int iadmm_gemm_nt_packed(int64_t M, int64_t Ni, int64_t K, const floa
   hipStream_t s = (hipStream_t)stream;
   return accumulate ? launch_gemm_nt_dma<true, true>(M, Ni, K, X, Wpk, out, s)
                     : launch_gemm_nt_dma<false, true>(M, Ni, K, X, Wpk, out, s);
+}
+
+extern "C" int iadmm_gemm_nt_packed_split(int64_t M, int64_t Ni, int64_t K, int64_t ksplit, const float* X,
+                                          const float* Wpk, float* slab, float* out, int accumulate, void* stream) {
+  if (M <= 0 || Ni <= 0 || K <= 0 || ksplit <= 0 || !X || !Wpk || !out) return IADMM_E_ARG;
+  if (ksplit == 1) return iadmm_gemm_nt_packed(M, Ni, K, X, Wpk, out, accumulate, stream);
+  if (!slab) return IADMM_E_ARG;
+  if (Ni > (1 << 20) || K > (1 << 20) || K * 256 * 4 > 0x7fffffffLL || ksplit > 65535) return IADMM_E_SIZE;
+  if (K % 16 || Ni % 4 || !aligned16(X) || !aligned16(Wpk) || !aligned16(slab) || !aligned16(out)) return IADMM_E_ALIGN;
+  const int64_t kpart = iadmm_gemm_nt_kpart(K, ksplit);
+  if ((K + kpart - 1) / kpart != ksplit) return IADMM_E_ARG;  // every split non-empty
+  const int ti = gemm_nt_tile(Ni);
+  const int64_t nit = (Ni + ti - 1) / ti, nrt = (M + 255) / 256;
+  if (nit * nrt > 0x7fffffffLL) return IADMM_E_SIZE;
+  const dim3 grid((unsigned)(nit * nrt), (unsigned)ksplit);
+  hipStream_t s = (hipStream_t)stream;
+  if (ti == 160) {
+    constexpr int lds = dma_ring_floats<5>() * 4;
+    IADMM_ALLOW_LDS(gemm_nt_dma_split_kernel<5>, lds);
+    hipLaunchKernelGGL(gemm_nt_dma_split_kernel<5>, grid, dim3(256), lds, s, M, (int)Ni, (int)K, (int)kpart, X, Wpk, slab);
+  } else {
+    constexpr int lds = dma_ring_floats<4>() * 4;
+    IADMM_ALLOW_LDS(gemm_nt_dma_split_kernel<4>, lds);
+    hipLaunchKernelGGL(gemm_nt_dma_split_kernel<4>, grid, dim3(256), lds, s, M, (int)Ni, (int)K, (int)kpart, X, Wpk, slab);
+  }
+  IADMM_CHECK_LAUNCH();
+  return launch_slab_reduce(M * Ni, ksplit, slab, out, accumulate, s);
+}
+
+extern "C" int64_t iadmm_gemm_nt_kpart(int64_t K, int64_t ksplit) {
+  if (K <= 0 || ksplit <= 0) return 0;
+  return ((K + ksplit - 1) / ksplit + 31) / 32 * 32;
 }
 
 extern "C" int64_t iadmm_gemm_tn_splits(int64_t M, int64_t rows_per_split) {

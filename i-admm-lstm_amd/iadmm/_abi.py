@@ -72,6 +72,8 @@ SIGNATURES = {
     "iadmm_gemm_packed_a_floats": (i64, [i64, i64]),
     "iadmm_gemm_pack_a": (cint, [i64, i64, vp, vp, vp]),
     "iadmm_gemm_nt_packed": (cint, [i64, i64, i64, vp, vp, vp, cint, vp]),
+    "iadmm_gemm_nt_kpart": (i64, [i64, i64]),
+    "iadmm_gemm_nt_packed_split": (cint, [i64, i64, i64, i64, vp, vp, vp, vp, cint, vp]),
     "iadmm_gemm_tn_splits": (i64, [i64, i64]),
     "iadmm_gemm_tn": (cint, [i64, i64, i64, i64, vp, vp, vp, vp, cint, vp]),
     "iadmm_slab_reduce": (cint, [i64, i64, vp, vp, cint, vp]),

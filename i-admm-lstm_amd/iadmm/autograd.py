@@ -33,10 +33,46 @@ def _end(tok):
         TIMER.stop(tok)
 
 
+class WindowGrads:
+    """Parameter-gradient accumulators shared by the IterationFn nodes of one chain of iterations (a
+    TBPTT window: each iteration's H comes out of the previous one's node).
+
+    r06: every node used to return its 16 parameter gradients to autograd, whose input buffers then
+    summed the T contributions per parameter (a 10-MB add per U gate, an add and a gather copy per
+    tensor per iteration: ~20 launches per iteration, 8 % of a batch-2 window).  Now each node adds
+    its contributions straight into these buffers -- through the reductions that produce them
+    (slab reduce with accumulate, the schedule backward's +=) -- and returns None for the
+    parameters; the chain's first node (``owner``), whose backward runs after every later node's,
+    returns the sums.  Autograd's input buffer kept the first contribution as is and added the next
+    ones in execution order (t = T-1 down to 0); the buffers here start from the first reduction
+    (accumulate = 0) and add in the same order, so the gradients are the same sums in the same order
+    (the per-iteration slices of dU_cat / dW3 are taken once, at the end)."""
+
+    __slots__ = ("key", "dUcat", "dW3", "dWh", "drho", "dalpha", "dbh")
+
+    def __init__(self, key):
+        self.key = key
+        self.reset()
+
+    def reset(self):
+        self.dUcat = self.dW3 = self.dWh = self.drho = self.dalpha = self.dbh = None
+
+
+def window_grads_for(H, params):
+    """(WindowGrads, owner) for an iteration whose hidden state is H: the chain's accumulators when H
+    came out of an IterationFn of the same parameters, else new ones owned by this iteration."""
+    key = tuple(id(q) for q in params)
+    prev = getattr(H.grad_fn, "iadmm_acc", None) if H.grad_fn is not None else None
+    if prev is not None and prev.key == key:
+        return prev, False
+    return WindowGrads(key), True
+
+
 class IterationFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, meta, x, y, z, xv, H, C, *params):
-        t, num_ineq, sigma, data, packed = meta
+        t, num_ineq, sigma, data, packed, acc, owner = meta
+        ctx.iadmm_acc, ctx.iadmm_owner = acc, owner
         p = dict(zip(PARAM_NAMES, params))
         Q, pv, A0, zl, zu = data
         B, n = x.shape
@@ -62,7 +98,8 @@ class IterationFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dxo, dyo, dzo, dxvo, dHn, dCn, _db, _dr):
         x, y, z, xv, H, C, g, r, xvo, scal, *params = ctx.saved_tensors
-        t, num_ineq, sigma, data, packed = ctx.meta
+        t, num_ineq, sigma, data, packed, _, _ = ctx.meta
+        acc = ctx.iadmm_acc
         p = dict(zip(PARAM_NAMES, params))
         Q, pv, A0, zl, zu = data
         B, n = x.shape
@@ -83,29 +120,46 @@ class IterationFn(torch.autograd.Function):
         k = _span("k:dH")
         dH = ops.gemm_nt_packed(dP, Ucat_pk, h).reshape(H.shape)
         _end(k)
+        need = {k: ctx.needs_input_grad[7 + i] for i, k in enumerate(PARAM_NAMES)}
         k = _span("k:dU")
-        dUcat = ops.gemm_tn(H.reshape(M, h), dP)
+        if any(need["U_" + q] for q in GATES):
+            if acc.dUcat is None:
+                acc.dUcat = ops.gemm_tn(H.reshape(M, h), dP)
+            else:
+                ops.gemm_tn(H.reshape(M, h), dP, out=acc.dUcat, accumulate=True)
         _end(k)
-        X3 = torch.stack([xv.reshape(M), g.reshape(M), torch.ones(M, device=x.device)], dim=1).contiguous()
-        dW3 = ops.gemm_tn(X3, dP, rows_per_split=512)                                 # [3, 4h], streaming
-        dWh = ops.slab_reduce(whslab).reshape(h, 1)
+        if any(need[q + g_] for q in ("W_", "b_") for g_ in GATES):
+            X3 = torch.stack([xv.reshape(M), g.reshape(M), torch.ones(M, device=x.device)], dim=1).contiguous()
+            if acc.dW3 is None:
+                acc.dW3 = ops.gemm_tn(X3, dP)                                          # [3, 4h], streaming
+            else:
+                ops.gemm_tn(X3, dP, out=acc.dW3, accumulate=True)
+        if need["W_h"]:
+            if acc.dWh is None:
+                acc.dWh = ops.slab_reduce(whslab)
+            else:
+                ops.slab_reduce(whslab, out=acc.dWh, accumulate=True)
         # 4. d(in) -> d(xv), dg ; 5. KKT backward
         dg = ops.in_reduce(inpart, dxv)
         kkt_ds = ops.kkt_bwd(Q, A0, xv, y, r, dg.reshape(B, n + m), sigma, scal, num_ineq, dxv, dx, dy, dz)
-        # 6. schedule scalars and b_h
-        drho = torch.zeros_like(p["rho"])
-        dalpha = torch.zeros_like(p["alpha"])
-        dbh = torch.zeros_like(p["b_h"])
+        # 6. schedule scalars and b_h (iadmm_sched_bwd adds into its outputs)
+        if acc.drho is None:
+            acc.drho = torch.zeros_like(p["rho"])
+            acc.dalpha = torch.zeros_like(p["alpha"])
+            acc.dbh = torch.zeros_like(p["b_h"])
         ops.sched_bwd(p["rho"].detach().contiguous(), p["alpha"].detach().contiguous(), t, upd_part, kkt_ds,
-                      drho, dalpha, dbh)
-        grads = {}
-        for gi, k in enumerate(GATES):
-            sl = slice(gi * h, (gi + 1) * h)
-            grads["W_" + k] = dW3[0:2, sl].contiguous()
-            grads["U_" + k] = dUcat[:, sl].contiguous()
-            grads["b_" + k] = dW3[2, sl].contiguous()
-        grads.update(W_h=dWh, b_h=dbh, rho=drho, alpha=dalpha)
-        pgrads = [grads[k] if ctx.needs_input_grad[7 + i] else None for i, k in enumerate(PARAM_NAMES)]
+                      acc.drho, acc.dalpha, acc.dbh)
+        pgrads = [None] * len(PARAM_NAMES)
+        if ctx.iadmm_owner:  # the chain's first iteration: every later node has added its share
+            grads = dict(W_h=None if acc.dWh is None else acc.dWh.reshape(h, 1), b_h=acc.dbh, rho=acc.drho,
+                         alpha=acc.dalpha)
+            for gi, q in enumerate(GATES):
+                sl = slice(gi * h, (gi + 1) * h)
+                grads["W_" + q] = None if acc.dW3 is None else acc.dW3[0:2, sl].contiguous()
+                grads["U_" + q] = None if acc.dUcat is None else acc.dUcat[:, sl].contiguous()
+                grads["b_" + q] = None if acc.dW3 is None else acc.dW3[2, sl].contiguous()
+            pgrads = [grads[k] if ctx.needs_input_grad[7 + i] else None for i, k in enumerate(PARAM_NAMES)]
+            acc.reset()  # (the buffers now belong to autograd; a retained graph's next backward starts anew)
         return (None, dx, dy, dz, dxv, dH, dC, *pgrads)
 
 

@@ -378,18 +378,76 @@ def gemm_pack_a(W):
     return Wpk
 
 
-def gemm_nt_packed(X, Wpk, Ni, out=None, accumulate=False):
-    """out[M,Ni] (+)= X[M,K] W[Ni,K]^T with W pre-packed by gemm_pack_a."""
+def _cu_count():
+    dev = torch.cuda.current_device()
+    n = _CU_COUNT.get(dev)
+    if n is None:
+        n = _CU_COUNT[dev] = int(torch.cuda.get_device_properties(dev).multi_processor_count)
+    return n
+
+
+_CU_COUNT = {}
+GEMM_FILL = 2  # workgroup slots per CU the small-M GEMM splits aim to fill (two 4-wave workgroups per CU)
+
+
+def _gemm_tile(Ni):
+    """csrc/gemm.hip gemm_nt_tile: 160-row output tiles when they pad Ni less than 128-row tiles."""
+    w128, w160 = -(-Ni // 128) * 128 - Ni, -(-Ni // 160) * 160 - Ni
+    return 160 if w160 < w128 else 128
+
+
+def gemm_nt_ksplit(M, Ni, K):
+    """K splits for gemm_nt_packed (r06): 1 while the output tiles alone fill GEMM_FILL workgroups per
+    CU; below that (the recipe's batch 2: M = 4000, 80 tiles) as many splits of >= 256 K as fit in one
+    round of those slots (6 of 544: 480 workgroups; 7 made 560 for 512 slots, a second round)."""
+    tiles = -(-Ni // _gemm_tile(Ni)) * -(-M // 256)
+    want = GEMM_FILL * _cu_count()
+    if K % 16 or tiles >= want:
+        return 1
+    ks = min(want // tiles, max(1, K // 256))  # one round of workgroups (560 of 512 slots ran two)
+    if ks <= 1:
+        return 1
+    kpart = int(_abi.lib().iadmm_gemm_nt_kpart(K, ks))
+    return -(-K // kpart)
+
+
+def gemm_nt_packed(X, Wpk, Ni, out=None, accumulate=False, ksplit=None):
+    """out[M,Ni] (+)= X[M,K] W[Ni,K]^T with W pre-packed by gemm_pack_a.  ``ksplit``: K splits summed in
+    split order (default gemm_nt_ksplit: 1 unless the output tiles leave CUs idle)."""
     M, K = X.shape
     out = empty(M, Ni, like=X) if out is None else out
-    _abi.call("iadmm_gemm_nt_packed", M, Ni, K, _p(X), _p(Wpk), _p(out), int(bool(accumulate)), _stream())
+    ks = gemm_nt_ksplit(M, Ni, K) if ksplit is None else int(ksplit)
+    if ks <= 1:
+        _abi.call("iadmm_gemm_nt_packed", M, Ni, K, _p(X), _p(Wpk), _p(out), int(bool(accumulate)), _stream())
+        return out
+    slab = empty(ks, M, Ni, like=X)
+    _abi.call("iadmm_gemm_nt_packed_split", M, Ni, K, ks, _p(X), _p(Wpk), _p(slab), _p(out), int(bool(accumulate)),
+              _stream())
     return out
 
 
-def gemm_tn(X, Y, rows_per_split=4096, out=None, accumulate=False):
-    """out[Ni,No] (+)= X[M,Ni]^T Y[M,No] (split over M, fixed-order reduction)."""
+def gemm_tn_rows_per_split(M, Ni, No, cap=4096):
+    """Row slices for gemm_tn (r06): ``cap`` rows (the r01-r05 default: 4096 on MFMA, 512 for the
+    skinny Ni <= 4 kernel) while the output tiles x slices fill GEMM_FILL workgroups per CU; fewer rows
+    per slice (>= 256 / 32, a multiple of 32) when they do not (the recipe's batch 2: M = 4000 rows,
+    65 output tiles -> 7 slices of 576 rows instead of 1 (one round of workgroups); the skinny d[W;b] GEMM 125 slices of 32
+    rows instead of 8 of 512)."""
+    if Ni <= 4:  # the streaming skinny kernel: 1024 columns x one slice per workgroup, 512-row slices
+        tiles, cap, floor = -(-No // 1024), 512, 32
+    else:
+        tiles, floor = -(-Ni // _gemm_tile(Ni)) * -(-No // 256), 256
+    ns = max(1, GEMM_FILL * _cu_count() // tiles)  # one round of workgroups
+    rps = -(-M // ns)
+    return int(min(cap, max(floor, -(-rps // 32) * 32)))
+
+
+def gemm_tn(X, Y, rows_per_split=None, out=None, accumulate=False):
+    """out[Ni,No] (+)= X[M,Ni]^T Y[M,No] (split over M, fixed-order reduction).  ``rows_per_split``:
+    default gemm_tn_rows_per_split."""
     M, Ni = X.shape
     No = Y.shape[1]
+    if rows_per_split is None:
+        rows_per_split = gemm_tn_rows_per_split(M, Ni, No)
     ns = int(_abi.lib().iadmm_gemm_tn_splits(M, rows_per_split))
     slab = empty(ns, Ni, No, like=X)
     out = empty(Ni, No, like=X) if out is None else out

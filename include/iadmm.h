@@ -274,6 +274,15 @@ int iadmm_gemm_pack_a(int64_t Ni, int64_t K, const float* W, float* Wpk, void* s
 int iadmm_gemm_nt_packed(int64_t M, int64_t Ni, int64_t K, const float* X, const float* Wpk, float* out,
                          int accumulate, void* stream);
 
+/* The packed form split over K (r06: small M, e.g. the recipe's batch 2 with 80 output tiles): split y
+ * takes K columns [kpart y, kpart (y + 1)), kpart = iadmm_gemm_nt_kpart(K, ksplit) (a multiple of 32;
+ * every split non-empty, IADMM_E_ARG otherwise), writes slab[ksplit][M][Ni] (caller-owned scratch),
+ * and the slabs are summed in split order into out (+= when accumulate).  ksplit = 1 is
+ * iadmm_gemm_nt_packed (slab unused).  K % 16 == 0 with ksplit > 1. */
+int64_t iadmm_gemm_nt_kpart(int64_t K, int64_t ksplit);
+int iadmm_gemm_nt_packed_split(int64_t M, int64_t Ni, int64_t K, int64_t ksplit, const float* X, const float* Wpk,
+                               float* slab, float* out, int accumulate, void* stream);
+
 /* out[Ni,No] (+)= X[M,Ni]^T . Y[M,No], split over M in slices of rows_per_split (multiple of 32):
  * slab[iadmm_gemm_tn_splits(M, rows_per_split)][Ni][No] is caller-owned scratch.  fp32 MFMA for
  * Ni > 4 (dU_cat = H^T dP); Ni <= 4 (d[W_x; b] = [xv, g, 1]^T dP) streams Y once on the VALU. */

@@ -17,7 +17,7 @@ import torch.nn as nn
 import iadmm_path  # noqa: F401
 from iadmm import ops
 from iadmm.kktop import KKTOperator
-from iadmm.autograd import IterationFn
+from iadmm.autograd import IterationFn, window_grads_for
 from iadmm.solver import PARAM_NAMES, PackedWeights, param_dict
 
 _GATES = ("i", "f", "o", "u")
@@ -94,10 +94,12 @@ class LSTM(nn.Module):
         m = y.shape[1]
         N = n + m
         flat = lambda a, k: a.float().reshape(B, k).contiguous()  # noqa: E731 (keeps autograd)
-        meta = (int(t), int(num_ineq), float(sigma), (Q, pv, A0, zlv, zuv), self._packed)
+        Hc = H_t.float().contiguous()
+        plist = [params[k] for k in PARAM_NAMES]
+        acc, owner = window_grads_for(Hc, plist)  # the window's shared parameter-gradient sums (r06)
+        meta = (int(t), int(num_ineq), float(sigma), (Q, pv, A0, zlv, zuv), self._packed, acc, owner)
         xo, yo, zo, xvo, Hn, Cn, btild, rho_vec = IterationFn.apply(
-            meta, flat(x, n), flat(y, m), flat(z, m), flat(xv, N), H_t.float().contiguous(),
-            C_t.float().contiguous(), *[params[k] for k in PARAM_NAMES])
+            meta, flat(x, n), flat(y, m), flat(z, m), flat(xv, N), Hc, C_t.float().contiguous(), *plist)
         A_tild = KKTOperator(Q, A0, sigma, ops.schedule(self.rho.detach().contiguous(),
                                                         self.alpha.detach().contiguous(), t), num_ineq)
         return (xo.unsqueeze(-1), yo.unsqueeze(-1), zo.unsqueeze(-1), xvo.unsqueeze(-1), Hn, Cn,

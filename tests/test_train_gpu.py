@@ -100,10 +100,18 @@ def test_gemm_nt_matches_fp64(M, Ni, K):
     assert rel_l2(acc, 2 * (X.double() @ W.double().T)) < tol
     if K % 4 == 0 and Ni % 4 == 0:  # the pre-packed A operand (same products, same order)
         Wpk = ops.gemm_pack_a(W.cuda())
-        pk = ops.gemm_nt_packed(X.cuda(), Wpk, Ni)
+        pk = ops.gemm_nt_packed(X.cuda(), Wpk, Ni, ksplit=1)
         assert torch.equal(pk, out)
-        pk = ops.gemm_nt_packed(X.cuda(), Wpk, Ni, out=pk, accumulate=True)
+        pk = ops.gemm_nt_packed(X.cuda(), Wpk, Ni, out=pk, accumulate=True, ksplit=1)
         assert torch.equal(pk, acc)
+        if K % 16 == 0:  # r06: split over K (small M), slabs summed in split order
+            for ks in sorted({ops.gemm_nt_ksplit(M, Ni, K), min(3, K // 16)}):
+                kpart = int(ops._abi.lib().iadmm_gemm_nt_kpart(K, ks))
+                ks = -(-K // kpart)
+                sp = ops.gemm_nt_packed(X.cuda(), Wpk, Ni, ksplit=ks)
+                assert rel_l2(sp, X.double() @ W.double().T) < tol, ks
+                sp2 = ops.gemm_nt_packed(X.cuda(), Wpk, Ni, out=sp.clone(), accumulate=True, ksplit=ks)
+                assert torch.equal(sp2, sp + sp), ks  # out + sum of slabs: the same adds
 
 
 @pytest.mark.parametrize("M,Ni,No", [(300, 40, 160), (5000, 130, 96), (4099, 3, 50), (5000, 136, 300), (2050, 800, 3200)])
@@ -115,3 +123,5 @@ def test_gemm_tn_matches_fp64(M, Ni, No):
     X, Y = torch.randn(M, Ni, generator=g), torch.randn(M, No, generator=g)
     out = ops.gemm_tn(X.cuda(), Y.cuda(), rows_per_split=1024)
     assert rel_l2(out, X.double().T @ Y.double()) < 5e-8 * M ** 0.5
+    auto = ops.gemm_tn(X.cuda(), Y.cuda())  # r06: rows per split by the fill policy
+    assert rel_l2(auto, X.double().T @ Y.double()) < 5e-8 * M ** 0.5
