@@ -2004,15 +2004,22 @@ static int lu_factor_blocks(int64_t B, int64_t N, float* A, int* piv, int* info,
   // (without a context, or with the interchanges as a pass of their own (gather = false), everything
   // runs in order on the caller's stream)
   iadmm_lu_ctx* side = gather && !paired ? ctx : nullptr;
+  // Under stream capture the critical path stays on the caller's (capturing) stream and the side
+  // strips fork from it directly (r06).  The eager hop s0 -> s1 -> s2 is a fork from a stream that
+  // joined the capture through another forked stream, and the HIP runtime python processes load --
+  // PyTorch's bundled libamdhip64 (ROCm 7.0.2), which this library binds to by soname -- crashes in
+  // hipStreamEndCapture on exactly that shape (tools/capture_probe.hip variant 2; variants 1, 9, 10,
+  // forks from the capture's origin only, capture and replay; the system HIP 7.2 runtime takes all of
+  // them: profiles/r06_capture_probe.txt).  r05 ran the whole factorization on one stream under
+  // capture instead; the captured graph now has the eager schedule's concurrency.  (Stream
+  // priorities do not carry into a graph, so s1's role is moot there.)
+  bool capturing = false;
   if (side) {
-    // Under stream capture every launch stays on the caller's stream (same factors, bit for bit):
-    // capturing the fork / join across the context's two streams crashed the HIP 7.2 runtime in
-    // hipStreamEndCapture (gpurun r05a, torch.cuda.graph around ops.lu_factor).
     hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
     IADMM_HIP_RC(hipStreamIsCapturing(s0, &cs));
-    if (cs != hipStreamCaptureStatusNone) side = nullptr;
+    capturing = cs != hipStreamCaptureStatusNone;
   }
-  if (side) {  // (nothing is enqueued on s1 before both calls succeed: a failure returns unforked)
+  if (side && !capturing) {  // (nothing is enqueued on s1 before both calls succeed: a failure returns unforked)
     IADMM_HIP_RC(hipEventRecord(side->ev0, s0));
     IADMM_HIP_RC(hipStreamWaitEvent(side->s1, side->ev0, 0));
     s = side->s1;
@@ -2124,8 +2131,10 @@ static int lu_factor_blocks(int64_t B, int64_t N, float* A, int* piv, int* info,
     }
   }
   if (side) {  // the caller's stream joins s1 -- and s2 directly if s1 has not -- on every path after the fork
-    const hipError_t e1 = hipEventRecord(side->ev1, s);
-    keep(e1 == hipSuccess ? hipStreamWaitEvent(s0, side->ev1, 0) : e1);
+    if (s != s0) {
+      const hipError_t e1 = hipEventRecord(side->ev1, s);
+      keep(e1 == hipSuccess ? hipStreamWaitEvent(s0, side->ev1, 0) : e1);
+    }
     if (pending) keep(hipStreamWaitEvent(s0, side->join, 0));
   }
   return rc;
@@ -2346,14 +2355,11 @@ extern "C" int iadmm_lu_factor_ex(int64_t B, int64_t N, float* A, int* piv, int*
   // batch of at least two instances per CU the two halves are factored concurrently on the context's
   // two streams -- the instances share nothing, so the factors are bit for bit those of one call, and
   // one half's latency-bound panel steps overlap the other half's updates (B = 1024, N = 2000: 75.8 ->
-  // 74.1 ms, profiles/r05_lu_split_ab.txt; four parts: 78.7).  Not under stream capture (see below).
-  bool split = ctx && pairs && gather && N <= kLeftDeferMaxN && N % 4 == 0 && aligned16(A) && B >= 512 &&
-               ws_bytes >= lu_ws_bytes(B / 2, N) + lu_ws_bytes(B - B / 2, N);
-  if (split) {
-    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-    IADMM_HIP_RC(hipStreamIsCapturing(s, &cs));
-    split = cs == hipStreamCaptureStatusNone;
-  }
+  // 74.1 ms, profiles/r05_lu_split_ab.txt; four parts: 78.7).  Both halves fork from the caller's stream
+  // by one event, which a stream capture takes as well (tools/capture_probe.hip variant 9; r06 -- r05
+  // kept captured factorizations on one stream).
+  const bool split = ctx && pairs && gather && N <= kLeftDeferMaxN && N % 4 == 0 && aligned16(A) && B >= 512 &&
+                     ws_bytes >= lu_ws_bytes(B / 2, N) + lu_ws_bytes(B - B / 2, N);
   if (!split) return run(0, B, static_cast<char*>(ws), s, ctx);
   const int64_t B0 = B / 2, B1 = B - B0;
   char* w1 = static_cast<char*>(ws) + lu_ws_bytes(B0, N);  // (16-B multiple)

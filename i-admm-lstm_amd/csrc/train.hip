@@ -533,12 +533,35 @@ __global__ void sched_bwd_kernel(const float* rho_param, const float* alpha_para
                                  float* drho, float* dalpha, float* dbh) {
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
   float ds = 0.f, da = 0.f, db = 0.f;
-  for (int k = 0; k < nblk; ++k) {
+  // (r06) loads issued eight partials at a time, adds in the same order: one memory latency per eight
+  // partials instead of per partial (27 us of a batch-2 iteration's 1.2 ms were this loop's chain)
+  int k = 0;
+  const bool al = (reinterpret_cast<uintptr_t>(upd_partials) & 15) == 0;
+  for (; al && k + 8 <= nblk; k += 8) {
+    float4 v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = *reinterpret_cast<const float4*>(upd_partials + 4 * (k + u));
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      ds += v[u].x;
+      da += v[u].y;
+      db += v[u].z;
+    }
+  }
+  for (; k < nblk; ++k) {
     ds += upd_partials[4 * k + 0];
     da += upd_partials[4 * k + 1];
     db += upd_partials[4 * k + 2];
   }
-  for (int64_t b = 0; b < B; ++b) ds += kkt_ds[b];
+  int64_t b = 0;
+  for (; b + 8 <= B; b += 8) {
+    float v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = kkt_ds[b + u];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) ds += v[u];
+  }
+  for (; b < B; ++b) ds += kkt_ds[b];
   const float s = sigmoidf_(rho_param[t]);
   const float sa = sigmoidf_(alpha_param[t]);
   drho[t] += ds * s * (1.f - s);

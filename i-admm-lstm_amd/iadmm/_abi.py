@@ -17,10 +17,13 @@ def _lib_path():
     the variant studies of tools/ (tools/lu_ab.py, tools/cellbwd_ab.py, ...); it is honoured only for a
     .so under the repository's tools/ or variants/ directory, so the product path cannot be swapped
     for an arbitrary library."""
+    own = os.path.join(_HERE, "libiadmm.so")
     alt = os.environ.get("IADMM_LIB_PATH")
     if not alt:
-        return os.path.join(_HERE, "libiadmm.so")
+        return own
     real = os.path.realpath(alt)
+    if real == os.path.realpath(own):
+        return own
     roots = [os.path.realpath(os.path.join(_REPO, d)) + os.sep for d in ("tools", "variants")]
     if not real.endswith(".so") or not any(real.startswith(r) for r in roots):
         raise RuntimeError(f"IADMM_LIB_PATH={alt!r}: variant libraries must be .so files under tools/ or variants/")

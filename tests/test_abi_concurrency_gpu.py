@@ -3,9 +3,10 @@ stream-ordered calls that are safe to capture in a hipGraph and to call from sev
 distinct streams, and run-to-run determinism of the kernels whose stores go through LDS stages.
 
 * Stage II (models/lu.py:26-35): ``ops.lu_factor`` + ``ops.lu_solve`` captured with
-  ``torch.cuda.graph`` and replayed (under capture every launch stays on the capturing stream) --
-  factors, pivots and solutions bitwise those of eager runs (N = 2000 paired blocks; N = 2500 rank-128
-  blocks, whose eager run uses the look-ahead);
+  ``torch.cuda.graph`` and replayed -- factors, pivots and solutions bitwise those of eager runs (N = 2000
+  paired blocks; N = 2500 rank-128 blocks with the look-ahead's side stream forked from the capturing
+  stream; N = 2000 at B = 512, the batch split's two streams; r06: captured graphs keep the eager
+  schedule's concurrency, tools/capture_probe.hip);
 * two Python threads factoring different batches on two streams at the same time, each with its own
   look-ahead context -- bitwise the serial results;
 * the look-ahead (context) path bitwise equal to the single-stream path (NULL context), for the
@@ -33,10 +34,10 @@ def _gpu():
 def _kkt_like(B, N, seed):
     """Random dense matrices with a zero (1,1) entry and a weak diagonal: real interchanges in every
     block."""
-    g = torch.Generator().manual_seed(seed)
-    K = torch.randn(B, N, N, generator=g)
+    g = torch.Generator(device="cuda").manual_seed(seed)
+    K = torch.randn(B, N, N, generator=g, device="cuda")
     K[:, 0, 0] = 0.0
-    return K.cuda(), torch.randn(B, N, generator=g).cuda()
+    return K, torch.randn(B, N, generator=g, device="cuda")
 
 
 def _factor_solve(K, b, lookahead=True, flags=0):
@@ -79,11 +80,11 @@ def test_lu_repeat_and_lookahead_bitwise(rank128):
 
 
 @pytest.mark.timeout(300)
-@pytest.mark.parametrize("N", [2000, 2500])
-def test_lu_graph_capture_replay_bitwise(N):
-    """N = 2000: paired blocks; N = 2500: rank-128 blocks, whose eager run forks the look-ahead."""
+@pytest.mark.parametrize("N,B", [(2000, 4), (2500, 4), (2000, 512)])
+def test_lu_graph_capture_replay_bitwise(N, B):
+    """N = 2000: paired blocks; N = 2500: rank-128 blocks with the look-ahead (its side stream forked
+    from the capturing stream); B = 512: the batch split over the context's two streams."""
     from iadmm import ops
-    B = 4
     K, b = _kkt_like(B, N, 12)
     eager = _factor_solve(K, b)
     torch.cuda.synchronize()

@@ -12,8 +12,17 @@
 //   7  6 with s2's join waited on s1 only after s1 forks the next s2 launch (not the LU's order: a check)
 //   8  6 with 80 KB of dynamic LDS per kernel and hipFuncSetAttribute called inside the capture, as
 //      lu_factor_blocks does (IADMM_ALLOW_LDS at the top of every call)
+//   9  the batch split's shape: s0 forks s1 and s2 by one event, kernels on both, both joined into s0
+//  10  the r06 look-ahead under capture: the critical path stays on s0, and every block forks s2 from
+//      s0 (kernel on s2, its join waited by s0 at the next block), as 5 without the s0 -> s1 hop
+// Finding (gpurun r06f): on torch's bundled HIP runtime (ROCm 7.0.2) variant 1 captures and variant 2
+// crashes in hipStreamEndCapture -- a fork from a stream that joined the capture through another
+// forked stream; on the system HIP 7.2 runtime all of 1-8 capture, instantiate and replay.
 //
-// Build: hipcc --offload-arch=gfx950 -O2 tools/capture_probe.hip -o tools/capture_probe.bin
+// Build: hipcc --offload-arch=gfx950 -O2 tools/capture_probe.hip -o /tmp/capture_probe  (system HIP 7.2, via
+// the binary's RPATH), or with -shared -fPIC -DPROBE_LIB into a library that tools/capture_probe_torch.py
+// loads into a python process after torch: it then runs on torch's bundled HIP runtime (ROCm 7.0.2),
+// the one libiadmm.so binds to in every python caller (same soname, loaded first).
 #include <hip/hip_runtime.h>
 #include <cstdio>
 #include <cstdlib>
@@ -54,7 +63,7 @@ struct Ctx {
 };
 
 static int make_ctx(Ctx& c) {
-  if (variant >= 3) {
+  if (variant >= 3 && variant <= 8) {
     int least = 0, greatest = 0;
     CK(hipDeviceGetStreamPriorityRange(&least, &greatest));
     CK(hipStreamCreateWithPriority(&c.s1, hipStreamNonBlocking, greatest));
@@ -65,11 +74,54 @@ static int make_ctx(Ctx& c) {
   }
   hipEvent_t* evs[4] = {&c.fork, &c.join, &c.ev0, &c.ev1};
   for (auto* e : evs) CK(variant >= 4 ? hipEventCreateWithFlags(e, hipEventDisableTiming) : hipEventCreate(e));
+  if (variant >= 9) {  // the LU context's priority streams
+    CK(hipStreamDestroy(c.s1));
+    CK(hipStreamDestroy(c.s2));
+    int least = 0, greatest = 0;
+    CK(hipDeviceGetStreamPriorityRange(&least, &greatest));
+    CK(hipStreamCreateWithPriority(&c.s1, hipStreamNonBlocking, greatest));
+    CK(hipStreamCreateWithPriority(&c.s2, hipStreamNonBlocking, least));
+  }
   return 0;
 }
 
 // The factorization's stream pattern over nb blocks on buffers a (critical path) and b (side work).
 static int pattern(const Ctx& c, hipStream_t s0, float* a, float* b, int n, int nb) {
+  if (variant == 9) {
+    CK(hipEventRecord(c.ev0, s0));
+    CK(hipStreamWaitEvent(c.s1, c.ev0, 0));
+    CK(hipStreamWaitEvent(c.s2, c.ev0, 0));
+    for (int k = 0; k < nb; ++k) {
+      launch(c.s1, a, n, (float)k);
+      launch(c.s2, b, n, (float)k);
+    }
+    CK(hipGetLastError());
+    CK(hipEventRecord(c.ev1, c.s1));
+    CK(hipStreamWaitEvent(s0, c.ev1, 0));
+    CK(hipEventRecord(c.join, c.s2));
+    CK(hipStreamWaitEvent(s0, c.join, 0));
+    return 0;
+  }
+  if (variant == 10) {
+    bool pending = false;
+    for (int k = 0; k < nb; ++k) {
+      launch(s0, a, n, (float)k);
+      if (pending) {
+        CK(hipStreamWaitEvent(s0, c.join, 0));
+        pending = false;
+      }
+      if (k + 1 < nb) {
+        CK(hipEventRecord(c.fork, s0));
+        CK(hipStreamWaitEvent(c.s2, c.fork, 0));
+        launch(c.s2, b, n, (float)k);
+        CK(hipEventRecord(c.join, c.s2));
+        pending = true;
+      }
+      CK(hipGetLastError());
+    }
+    if (pending) CK(hipStreamWaitEvent(s0, c.join, 0));
+    return 0;
+  }
   if (variant >= 8) CK(hipFuncSetAttribute((const void*)bump_lds, hipFuncAttributeMaxDynamicSharedMemorySize, 80 * 1024));
   CK(hipEventRecord(c.ev0, s0));
   CK(hipStreamWaitEvent(c.s1, c.ev0, 0));
@@ -105,8 +157,8 @@ static int pattern(const Ctx& c, hipStream_t s0, float* a, float* b, int n, int 
   return 0;
 }
 
-int main(int argc, char** argv) {
-  variant = argc > 1 ? std::atoi(argv[1]) : 1;
+extern "C" int capture_probe_run(int v) {
+  variant = v;
   const int n = 1 << 16, nb = 20;
   float *a = nullptr, *b = nullptr;
   CK(hipMalloc(&a, n * sizeof(float)));
@@ -117,7 +169,7 @@ int main(int argc, char** argv) {
   CK(hipStreamCreateWithFlags(&s0, hipStreamNonBlocking));
   Ctx c;
   if (make_ctx(c)) return 1;
-  if (variant >= 6 && pattern(c, s0, a, b, n, nb)) return 1;  // eager warm-up with the same objects
+  if (variant >= 6 && pattern(c, s0, a, b, n, nb)) return 1;  // eager warm-up with the same objects (6-10)
   CK(hipStreamSynchronize(s0));
   std::printf("variant %d: begin capture\n", variant);
   std::fflush(stdout);
@@ -140,3 +192,7 @@ int main(int argc, char** argv) {
   CK(hipGraphDestroy(graph));
   return 0;
 }
+
+#ifndef PROBE_LIB
+int main(int argc, char** argv) { return capture_probe_run(argc > 1 ? std::atoi(argv[1]) : 1); }
+#endif
