@@ -247,7 +247,13 @@ IADMM_DEV void panel_finish(float* Ab, int N, int K0, int k0, int nb, int cend, 
 // leaving registers.
 // DIAG (tools/lupanelbench.hip only): 1 = no column steps (identity interchanges), 2 = no
 // panel_finish, 3 = neither (the panel's load and store alone).
-template <int M, int NB, int NT, int DIAG = 0>
+// PRE (r06; 16-wide staged panels that are not the first of their 64-column half): the rank-16 update
+// of this panel's columns by the previous panel of the half -- A[k0 + r][k0 + c] -= sum_l L[k0 + r][k0 -
+// 16 + l] U[k0 - 16 + l][k0 + c], the previous panel_finish's U12 rows -- is applied here as the rows
+// arrive, in lu_update_block_vec_kernel's fmaf order (factors bit for bit those of the separate
+// update), so the in-half update after the previous panel skips these 16 columns: the columns are
+// read once and written once instead of twice each, and the half's last update launch goes away.
+template <int M, int NB, int NT, int DIAG = 0, bool PRE = false>
 __global__ __launch_bounds__(NT, NT <= 256 ? (M <= 6 ? 4 : 2) : 1) void lu_panel_kernel(int N, int K0, int k0, int cend, float* A,
                                                                          int* piv, int* info) {
   constexpr int kNB = NB, kLuThreads = NT, NWV = NT / 64;
@@ -283,6 +289,8 @@ __global__ __launch_bounds__(NT, NT <= 256 ? (M <= 6 ? 4 : 2) : 1) void lu_panel
   // rows >= R read as zero (every use below is masked); the range ends at the panel's last row
   const __amdgpu_buffer_rsrc_t prs =
       __builtin_amdgcn_make_buffer_rsrc(Ab + (size_t)k0 * N + k0, 0, ((R - 1) * N + kNB) * 4, 0x00020000);
+  static_assert(!PRE || (NT == 256 && NB == 16), "PRE: staged 16-wide panels only");
+  __shared__ __attribute__((aligned(16))) float Up[PRE ? kNB : 1][PRE ? kNB : 1];
   if (staged) {
     // lane l of instruction i of block m: block row 16 i + (l >> 2), stage position l & 3, source
     // chunk (l & 3) ^ ((l >> 4) & 3)
@@ -295,6 +303,50 @@ __global__ __launch_bounds__(NT, NT <= 256 ? (M <= 6 ? 4 : 2) : 1) void lu_panel
     };
     const unsigned rb = (unsigned)(uintptr_t)(lds_cf4*)(const f4v*)&pst[wave][0][lane * kNB];
     const int sr = (lane >> 2) & 3;
+    if constexpr (PRE) {
+      // U (16 x 16) to LDS; per 64-row block, this block's A rows into stage buffer 0 and the same rows'
+      // L (the previous panel's 16 columns) into buffer 1, one block in flight (the panels are not bound
+      // by their load latency: profiles/r06_lu_ab_panel_asm_reads_rejected.txt)
+      Up[tid >> 4][tid & 15] = Ab[(size_t)(k0 - kNB + (tid >> 4)) * N + k0 + (tid & 15)];
+      __syncthreads();
+      const __amdgpu_buffer_rsrc_t lrs =
+          __builtin_amdgcn_make_buffer_rsrc(Ab + (size_t)k0 * N + k0 - kNB, 0, ((R - 1) * N + kNB) * 4, 0x00020000);
+#pragma unroll
+      for (int m = 0; m < M; ++m) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(prs, (lds_void*)(&pst[wave][0][i * 256]), 16, vo,
+                                                   (kLuThreads * m + 16 * i) * N * 4, 0, 0);
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(lrs, (lds_void*)(&pst[wave][1][i * 256]), 16, vo,
+                                                   (kLuThreads * m + 16 * i) * N * 4, 0, 0);
+        }
+        vm_wait<0>();
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          const f4v v = *(lds_cf4*)(uintptr_t)(rb + (unsigned)(((c ^ sr) * 4) * 4));
+          a[m][4 * c] = v.x; a[m][4 * c + 1] = v.y; a[m][4 * c + 2] = v.z; a[m][4 * c + 3] = v.w;
+        }
+        const unsigned lb = rb + (unsigned)(64 * kNB * 4);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {  // L[row][4q .. 4q + 4)
+          const f4v lq = *(lds_cf4*)(uintptr_t)(lb + (unsigned)(((q ^ sr) * 4) * 4));
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const float lv = e == 0 ? lq.x : (e == 1 ? lq.y : (e == 2 ? lq.z : lq.w));
+            const int li = 4 * q + e;
+#pragma unroll
+            for (int c4 = 0; c4 < 4; ++c4) {
+              const f4v u = *reinterpret_cast<const f4v*>(&Up[li][4 * c4]);
+              a[m][4 * c4] = fmaf(-lv, u.x, a[m][4 * c4]);
+              a[m][4 * c4 + 1] = fmaf(-lv, u.y, a[m][4 * c4 + 1]);
+              a[m][4 * c4 + 2] = fmaf(-lv, u.z, a[m][4 * c4 + 2]);
+              a[m][4 * c4 + 3] = fmaf(-lv, u.w, a[m][4 * c4 + 3]);
+            }
+          }
+        }
+        __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): both buffers read before the next block refills them
+      }
+    } else {
     issue(0);
     if (M > 1) issue(1);
 #pragma unroll
@@ -310,6 +362,7 @@ __global__ __launch_bounds__(NT, NT <= 256 ? (M <= 6 ? 4 : 2) : 1) void lu_panel
         __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this buffer's reads done before it refills
         issue(m + 2);
       }
+    }
     }
   } else {
 #pragma unroll
@@ -592,7 +645,9 @@ __global__ __launch_bounds__(256) void lu_update_block_kernel(int N, int k0, int
 // 16-B aligned rows): 16-B accesses, and only as many threads per row as the width needs (the
 // generic kernel sizes every launch for the widest update and clamps the rest onto repeated
 // loads).  Same operations in the same order per element as lu_update_block_kernel.
-template <int NB, int W>
+// CO (r06): the update's columns start CO past the rows' start, k0 + NB + CO (CO = NB: the next panel
+// applies its own columns' share itself, lu_panel_kernel PRE)
+template <int NB, int W, int CO = 0>
 __global__ __launch_bounds__(256) void lu_update_block_vec_kernel(int N, int k0, float* A) {
   constexpr int kW4 = W / 4, kNB4 = NB / 4;
   constexpr int kAq = kUpdRows * kW4 / 256;              // float4 of A per thread
@@ -603,8 +658,8 @@ __global__ __launch_bounds__(256) void lu_update_block_vec_kernel(int N, int k0,
   __shared__ float Ls[kUpdRows][NB + 1];
   const int tid = threadIdx.x;
   float* Ab = A + blockIdx.x * (size_t)N * N;
-  const int c0 = k0 + NB;
-  const int r0 = c0 + blockIdx.y * kUpdRows;
+  const int c0 = k0 + NB + CO;
+  const int r0 = k0 + NB + blockIdx.y * kUpdRows;
   const int rows = min(kUpdRows, N - r0);
   float4 u[kUq], l[kLq], a[kAq];
 #pragma unroll
@@ -1875,18 +1930,36 @@ using namespace iadmm;
 static int lu_factor_half(int64_t B, int64_t N, int K0, int cend, float* A, int* piv, int* info, hipStream_t s) {
   const bool vec = (N % 4 == 0) && aligned16(A);
   if (N <= kPanelMaxM * kLuThreads) {
+    // fuse (r06): in a full 64-column half with 16-B rows, each panel after the first applies the
+    // previous panel's update to its own 16 columns (lu_panel_kernel PRE), and the in-half update
+    // covers only the columns beyond the next panel: 48 + 32 + 16 updated columns per half become
+    // 32 + 16, and the half's last update launch goes away
+    const bool fuse = vec && cend - K0 == kBlk;
     for (int k0 = K0; k0 < cend; k0 += kNB) {
       const int R = (int)N - k0;
       const dim3 g((unsigned)B), t(kLuThreads);
-      if (R <= kLuThreads) hipLaunchKernelGGL((lu_panel_kernel<1, kNB, kLuThreads>), g, t, 0, s, (int)N, K0, k0, cend, A, piv, info);
-      else if (R <= 2 * kLuThreads) hipLaunchKernelGGL((lu_panel_kernel<2, kNB, kLuThreads>), g, t, 0, s, (int)N, K0, k0, cend, A, piv, info);
-      else if (R <= 4 * kLuThreads) hipLaunchKernelGGL((lu_panel_kernel<4, kNB, kLuThreads>), g, t, 0, s, (int)N, K0, k0, cend, A, piv, info);
-      else if (R <= 6 * kLuThreads) hipLaunchKernelGGL((lu_panel_kernel<6, kNB, kLuThreads>), g, t, 0, s, (int)N, K0, k0, cend, A, piv, info);
-      else hipLaunchKernelGGL((lu_panel_kernel<kPanelMaxM, kNB, kLuThreads>), g, t, 0, s, (int)N, K0, k0, cend, A, piv, info);
+      const bool pre = fuse && k0 > K0;
+#define IADMM_PANEL(MM)                                                                                             \
+  {                                                                                                               \
+    if (pre) hipLaunchKernelGGL((lu_panel_kernel<MM, kNB, kLuThreads, 0, true>), g, t, 0, s, (int)N, K0, k0, cend, A, piv, info); \
+    else hipLaunchKernelGGL((lu_panel_kernel<MM, kNB, kLuThreads>), g, t, 0, s, (int)N, K0, k0, cend, A, piv, info);        \
+  }
+      if (R <= kLuThreads) IADMM_PANEL(1)
+      else if (R <= 2 * kLuThreads) IADMM_PANEL(2)
+      else if (R <= 4 * kLuThreads) IADMM_PANEL(4)
+      else if (R <= 6 * kLuThreads) IADMM_PANEL(6)
+      else IADMM_PANEL(kPanelMaxM)
+#undef IADMM_PANEL
       IADMM_CHECK_LAUNCH();
       const int c0 = k0 + kNB;
       if (c0 < cend) {
-        lu_update_block<kNB>(B, N, k0, cend, A, vec, s);
+        if (!fuse) {
+          lu_update_block<kNB>(B, N, k0, cend, A, vec, s);
+        } else if (cend - c0 > kNB) {  // the columns beyond the next panel
+          const dim3 grid((unsigned)B, (unsigned)((N - c0 + kUpdRows - 1) / kUpdRows));
+          if (cend - c0 == 48) hipLaunchKernelGGL((lu_update_block_vec_kernel<kNB, 32, kNB>), grid, dim3(256), 0, s, (int)N, k0, A);
+          else hipLaunchKernelGGL((lu_update_block_vec_kernel<kNB, 16, kNB>), grid, dim3(256), 0, s, (int)N, k0, A);
+        }
         IADMM_CHECK_LAUNCH();
       }
     }
