@@ -169,3 +169,29 @@ def test_lib_path_override_limited_to_variant_dirs(tmp_path):
     r = subprocess.run([sys.executable, "-c", code + "; print(_abi.LIB_PATH)"], cwd=REPO, env=env,
                        capture_output=True, text=True)
     assert r.returncode == 0 and r.stdout.strip().endswith("iadmm/libiadmm.so"), r.stderr
+
+
+def test_small_m_gemm_split_policy():
+    """r06: the split counts of the training GEMMs (iadmm/ops.py) at the recipe's batch 2 and the
+    config-5 micro-batch, with the CU count given; the K-part size query is a host function."""
+    from iadmm import ops
+    lib = _abi.lib()
+    assert lib.iadmm_gemm_nt_kpart(3200, 6) == 544 and lib.iadmm_gemm_nt_kpart(3200, 1) == 3200
+    assert lib.iadmm_gemm_nt_kpart(48, 3) == 32 and lib.iadmm_gemm_nt_kpart(0, 3) == 0
+    saved = dict(ops._CU_COUNT)
+    dev = ops.torch.cuda.current_device
+    try:
+        ops.torch.cuda.current_device = lambda: 0
+        ops._CU_COUNT[0] = 256
+        # batch 2 (M = 4000 rows): one round of 512 workgroup slots
+        assert ops.gemm_nt_ksplit(4000, 800, 3200) == 6          # 80 tiles x 6 = 480
+        assert ops.gemm_tn_rows_per_split(4000, 800, 3200) == 576  # 65 tiles x 7 slices = 455
+        assert ops.gemm_tn_rows_per_split(4000, 3, 3200) == 32
+        # config-5 micro-batch (M = 256000): the r01-r05 splits, bitwise-unchanged gradients
+        assert ops.gemm_nt_ksplit(256000, 800, 3200) == 1
+        assert ops.gemm_tn_rows_per_split(256000, 800, 3200) == 4096
+        assert ops.gemm_tn_rows_per_split(256000, 3, 3200) == 512
+    finally:
+        ops.torch.cuda.current_device = dev
+        ops._CU_COUNT.clear()
+        ops._CU_COUNT.update(saved)

@@ -65,3 +65,26 @@ def test_resume_state_reloads_weights_only_after_np_best_loss(tmp_path):
     stopper.best_loss = None
     main.save_resume_state(path, model, opt, 4, stopper)
     assert torch.load(path, weights_only=True)["best_loss"] is None
+
+
+def test_synthetic_instances_cached_across_epochs():
+    """r06: main.py generates each synthetic instance once and reuses it in later epochs; the cached
+    instance is the one the generator makes (deterministic per seed and index), and callers get copies."""
+    import argparse
+    import torch
+    main._SYNTH_CACHE.clear()
+    main._SYNTH_CACHE_BYTES[0] = 0
+    args = argparse.Namespace(num_ineq=3, num_eq=2, num_var=6, synthetic=True, seed=100017)
+    d1 = main._instances(args, [4, 7], "cpu")
+    assert len(main._SYNTH_CACHE) == 2 and main._SYNTH_CACHE_BYTES[0] > 0
+    d2 = main._instances(args, [7, 4], "cpu")
+    assert len(main._SYNTH_CACHE) == 2
+    assert torch.equal(d1["Q"][0], d2["Q"][1]) and torch.equal(d1["A0"][1], d2["A0"][0])
+    from iadmm import data as qpdata
+    ref = qpdata.make_qp_batch(6, 3, 2, 1, first_index=7, seed=100017, device="cpu")
+    for k in ("Q", "p", "A0", "zl", "zu"):
+        assert torch.equal(d1[k][1:2], ref[k]), k
+    d2["Q"].zero_()  # a caller's tensors are not the cache's
+    assert torch.equal(main._instances(args, [4], "cpu")["Q"][0], d1["Q"][0])
+    main._SYNTH_CACHE.clear()
+    main._SYNTH_CACHE_BYTES[0] = 0
